@@ -1,0 +1,221 @@
+"""bench.py -- burn-proofs/sec of the MI355X STARK prover (BASELINE.json metric).
+
+One step = one batch of PER_GPU burn proofs per GPU (2^16-step trace, blowup 8, the reference's
+ProofOptions 42/8/4/None/8/31): BASELINE configs[2] at N=1, configs[3] (512 proofs on 8 GPUs)
+at N=8. Rank 0 holds the batch inputs and the proofs: it scatters packed inputs to the ranks and
+gathers the proof bytes back over RCCL (torch.distributed "nccl" backend), the only exchange
+step of the path; each rank proves its shard with libxfgstark.so (weak scaling).
+
+Prints ONE JSON line (rank 0) with `roofline` (trace-LDE kernel pair, HIP-event timed on the
+prover's stream) and `cpu_baseline` (the oracle C restatement, 1 thread, faithful per-row
+Keccak mode, bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "xfg-stark_amd"))
+sys.path.insert(0, ROOT)
+
+import synthetic  # noqa: E402
+
+LOG_N = 16
+BLOWUP = 8
+WIDTH = 7
+REC = 128  # packed input record bytes
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def pack_inputs(kws):
+    """[count, REC] uint8 records: burn u64, mint u64, tx 32, recipient 20, secret 32, ids 3xu32"""
+    import numpy as np
+    out = np.zeros((len(kws), REC), dtype=np.uint8)
+    for i, kw in enumerate(kws):
+        b = bytearray()
+        b += kw["burn_amount"].to_bytes(8, "little") + kw["mint_amount"].to_bytes(8, "little")
+        b += kw["tx_prefix_hash"] + kw["recipient_address"].ljust(20, b"\0")[:20] + kw["secret"].ljust(32, b"\0")[:32]
+        b += kw["network_id"].to_bytes(4, "little") + kw["target_chain_id"].to_bytes(4, "little")
+        b += kw["commitment_version"].to_bytes(4, "little")
+        out[i, :len(b)] = np.frombuffer(bytes(b), dtype=np.uint8)
+    return out
+
+
+def unpack_inputs(arr):
+    res = []
+    for r in arr:
+        b = bytes(r.tolist())
+        res.append(dict(burn_amount=int.from_bytes(b[0:8], "little"), mint_amount=int.from_bytes(b[8:16], "little"),
+                        tx_prefix_hash=b[16:48], recipient_address=b[48:68], secret=b[68:100],
+                        network_id=int.from_bytes(b[100:104], "little"),
+                        target_chain_id=int.from_bytes(b[104:108], "little"),
+                        commitment_version=int.from_bytes(b[108:112], "little")))
+    return res
+
+
+def sharded_step(prove_fn, all_inputs, rank, world, per_rank, device, dist):
+    """scatter packed inputs from rank 0, prove the local shard, gather proof bytes to rank 0.
+    Returns the list of proofs (bytes) on rank 0, None elsewhere."""
+    import numpy as np
+    import torch
+    if world == 1:
+        return prove_fn(all_inputs)
+    if rank == 0:
+        packed = torch.from_numpy(pack_inputs(all_inputs)).to(device).view(world, per_rank, REC)
+        chunks = list(packed.unbind(0))
+    else:
+        chunks = None
+    local = torch.empty((per_rank, REC), dtype=torch.uint8, device=device)
+    dist.scatter(local, chunks, src=0)
+    proofs = prove_fn(unpack_inputs(local.cpu().numpy()))
+    lens = torch.tensor([len(p) for p in proofs], dtype=torch.int64, device=device)
+    maxlen = torch.tensor([max(len(p) for p in proofs)], dtype=torch.int64, device=device)
+    dist.all_reduce(maxlen, op=dist.ReduceOp.MAX)
+    L = int(maxlen.item())
+    buf = np.zeros((per_rank, L), dtype=np.uint8)
+    for i, p in enumerate(proofs):
+        buf[i, :len(p)] = np.frombuffer(p, dtype=np.uint8)
+    tbuf = torch.from_numpy(buf).to(device)
+    glens = [torch.empty_like(lens) for _ in range(world)] if rank == 0 else None
+    gbufs = [torch.empty_like(tbuf) for _ in range(world)] if rank == 0 else None
+    dist.gather(lens, glens, dst=0)
+    dist.gather(tbuf, gbufs, dst=0)
+    if rank != 0:
+        return None
+    out = []
+    for r in range(world):
+        lr, br = glens[r].cpu().numpy(), gbufs[r].cpu().numpy()
+        out += [bytes(br[i, :lr[i]]) for i in range(per_rank)]
+    return out
+
+
+def cpu_baseline(seconds=10.0):
+    """oracle C restatement, single thread, faithful mode (per-row Keccak like the reference)"""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    n = 1 << LOG_N
+    done, t0 = 0, time.perf_counter()
+    while True:
+        kw = synthetic.burn_inputs(10_000 + done)
+        st, air = O.air_from_inputs(kw["burn_amount"], kw["mint_amount"], kw["tx_prefix_hash"],
+                                    kw["recipient_address"], kw["secret"])
+        st, proof = O.prove(air, n, O.options(), faithful=True)
+        assert st == 0
+        done += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": done / el, "unit": "proofs/s", "cores": 1, "kind": "port",
+            "sample": f"{done} proofs (2^16 steps, blowup 8) by oracle/liboracle.so in {el:.1f}s, 1 thread, "
+                      "faithful per-row Keccak (src/burn_mint_air.rs:264,376)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--per-gpu", type=int, default=64)
+    ap.add_argument("--log-n", type=int, default=LOG_N)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+    device = torch.device("cuda", local_rank)
+
+    import xfgstark
+    prover = xfgstark.XfgBurnMintProver(device=local_rank)
+    n = 1 << args.log_n
+    per = args.per_gpu
+
+    def prove_fn(kws):
+        res = prover.prove_batch(kws, trace_length=n)
+        for r in res:
+            if isinstance(r, Exception):
+                raise r
+        return [r.to_bytes() for r in res]
+
+    def step(idx):
+        base = idx * per * world
+        inputs = [synthetic.burn_inputs(base + i) for i in range(per * world)] if rank == 0 else None
+        return sharded_step(prove_fn, inputs, rank, world, per, device, dist)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for i in range(args.warmup):
+        step(i)
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        out = step(args.warmup + i)
+    barrier()
+    el = time.perf_counter() - t0
+    el_t = torch.tensor([el], dtype=torch.float64, device=device)
+    if dist is not None:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+    el = float(el_t.item())
+    if rank == 0:
+        assert out is not None and len(out) == per * world
+
+    # ---- roofline: trace LDE kernel pair, algorithmic bytes 8*w*(n+N) per proof
+    lde_ms = prover.bench_lde(per, n, BLOWUP, 10)
+    lde_bytes = 8 * WIDTH * (n + n * BLOWUP) * per
+    achieved = lde_bytes / (lde_ms * 1e-3) / 1e9
+    prover.set_timing(True)
+    prover_stage = {}
+    if rank == 0:
+        prover.prove_batch([synthetic.burn_inputs(i) for i in range(per)], trace_length=n)
+        prover_stage = {k: round(v, 3) for k, v in prover.stage_times().items()}
+    prover.set_timing(False)
+
+    if rank == 0:
+        total = per * world * args.steps
+        line = {
+            "metric": "burn-proofs/sec (2^16-step trace, blowup=8)",
+            "value": total / el,
+            "unit": "proofs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": el / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic",
+            "config": {
+                "workload": f"batch of {per} burn proofs per GPU (configs[2]; configs[3] = 512 proofs on 8 GPUs)",
+                "trace_length": n, "blowup": BLOWUP, "proof_options": "42/8/4/None/8/31",
+                "proofs_per_step": per * world,
+                "parallelism": f"dp{world} (independent proofs; RCCL scatter of inputs, gather of proof bytes)",
+            },
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
+                         "kernel": "trace LDE (ntt_cols_kernel + ntt_rows_kernel), 7 columns x "
+                                   f"{per} proofs, {lde_ms:.3f} ms/launch-set, {lde_bytes} algorithmic B"},
+            "stage_ms_one_batch": prover_stage,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    prover.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,120 @@
+/*
+ * xfg_stark.h -- C ABI of the MI355X-native XFG burn-proof STARK prover (libxfgstark.so).
+ *
+ * Drop-in boundary for the reference's proving path. Rust is not available in this build
+ * environment, so the host side above this ABI is C++ (inside the .so) and the reference-side
+ * binding a Rust maintainer would add is shown in INTEGRATION.md. Every entry point replaces a
+ * reference interface:
+ *
+ *   xfg_prove_burn_mint  <- XfgBurnMintProver::prove_burn_mint      src/burn_mint_prover.rs:62-129
+ *                           (validate_inputs :132-180, secret_to_field_element :195-208,
+ *                            compute_recipient_hash :211-221, air.prove(trace) :124-126)
+ *   xfg_prove_trace      <- <XfgBurnMintAir as winterfell::Prover>::prove(trace)
+ *                           src/burn_mint_air.rs:479-531 (ExecutionTrace-level entry; trace layout
+ *                           of build_trace :442-476, column-major)
+ *   xfg_prove_batch      <- the serial loops of the reference callers (e.g. benchmark harness
+ *                           src/benchmarks/mod.rs:301-342, BatchBurnMintVerifier's pattern
+ *                           src/burn_mint_verifier.rs:326-338) -- independent proofs, one launch set
+ *   xfg_default_options  <- XfgBurnMintProver::new(_) ProofOptions::new(42, 8, 4, None, 8, 31)
+ *                           src/burn_mint_prover.rs:27-41 (argument order: queries, blowup,
+ *                           grinding, extension, FRI folding, FRI remainder max degree)
+ *   xfg_proof_size_bound <- XfgBurnMintProver::get_proof_size  src/burn_mint_prover.rs:224-227
+ *   xfg_last_error       <- XfgStarkError::CryptoError(String) text  src/burn_mint_prover.rs:143-177
+ *
+ * Output bytes are the proof's `StarkProof::to_bytes()` serialisation as restated in DESIGN.md
+ * ("Proof format"); the caller owns all host buffers, the library owns device memory (pooled per
+ * context). `out == NULL` (or *out_len too small) returns the required size in *out_len.
+ * A context is bound to one HIP device and one stream; use one context per thread.
+ */
+#ifndef XFG_STARK_H
+#define XFG_STARK_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct xfg_ctx xfg_ctx;
+
+typedef enum {
+    XFG_OK = 0,
+    XFG_INVALID_BURN_AMOUNT = 1, /* burn not 8,000,000 or 8,000,000,000 atomic units */
+    XFG_MINT_MISMATCH = 2,       /* mint != burn (1:1) */
+    XFG_ZERO_TX_HASH = 3,        /* u64 LE of tx_prefix_hash[0..8] == 0 */
+    XFG_BAD_RECIPIENT_LEN = 4,   /* recipient address not 20 bytes */
+    XFG_SHORT_SECRET = 5,        /* secret shorter than 8 bytes (reference: error <4, panic 4..7) */
+    XFG_PROVER_ERROR = 6,        /* Winterfell prover error / unsupported options */
+    XFG_DEVICE_ERROR = 7,        /* HIP runtime failure */
+    XFG_BUFFER_TOO_SMALL = 8,
+    XFG_INVALID_ARGUMENT = 9
+} xfg_status;
+
+/* winterfell::ProofOptions (0.8) */
+typedef struct {
+    uint32_t num_queries;
+    uint32_t blowup_factor;
+    uint32_t grinding_factor;
+    uint32_t field_extension; /* 1 = FieldExtension::None */
+    uint32_t fri_folding_factor;
+    uint32_t fri_remainder_max_degree;
+} xfg_options;
+
+/* arguments of prove_burn_mint (src/burn_mint_prover.rs:62-72) */
+typedef struct {
+    uint64_t burn_amount;
+    uint64_t mint_amount;
+    uint8_t tx_prefix_hash[32];
+    const uint8_t* recipient_address;
+    size_t recipient_len;
+    const uint8_t* secret;
+    size_t secret_len;
+    uint32_t network_id;
+    uint32_t target_chain_id;
+    uint32_t commitment_version;
+} xfg_burn_inputs;
+
+/* AIR instance for ExecutionTrace-level proving: BurnMintPublicInputs::to_elements
+ * (src/burn_mint_air.rs:54-71) + the two Keccak-derived constants (:124-133, :174-202) */
+typedef struct {
+    uint64_t pub_inputs[12];
+    uint64_t nullifier;
+    uint64_t commitment;
+} xfg_air_consts;
+
+xfg_ctx* xfg_ctx_create(int device_id);
+void xfg_ctx_destroy(xfg_ctx* ctx);
+int xfg_default_options(xfg_options* out);
+/* length of the error text of the last failing call on ctx (copied NUL-terminated into buf) */
+int xfg_last_error(const xfg_ctx* ctx, char* buf, size_t len);
+size_t xfg_proof_size_bound(uint64_t trace_length, const xfg_options* opts);
+
+/* prove_burn_mint; trace_length 0 -> 64 (the reference's fixed TraceInfo::new(7, 64)) */
+int xfg_prove_burn_mint(xfg_ctx* ctx, const xfg_burn_inputs* in, uint64_t trace_length, const xfg_options* opts,
+                        uint8_t* out, size_t* out_len);
+/* prove over a caller-supplied execution trace, column-major [width][n], width must be 7 */
+int xfg_prove_trace(xfg_ctx* ctx, const uint64_t* trace, uint32_t width, uint64_t n, const xfg_air_consts* air,
+                    const xfg_options* opts, uint8_t* out, size_t* out_len);
+/* batch of independent proofs on this context's device; statuses[i] per proof, returns XFG_OK if
+ * the batch ran (individual proofs may still carry validation errors) */
+int xfg_prove_batch(xfg_ctx* ctx, uint32_t count, const xfg_burn_inputs* inputs, uint64_t trace_length,
+                    const xfg_options* opts, uint8_t* const* outs, size_t* out_lens, int* statuses);
+
+/* AIR constants from raw inputs (marshalling + Keccak, host); returns a validation status */
+int xfg_burn_air_consts(const xfg_burn_inputs* in, xfg_air_consts* out);
+
+/* ---- instrumentation (benchmarks / parity tests) ---- */
+/* per-stage device milliseconds of the last prove call when timing is enabled (returns count) */
+int xfg_set_timing(xfg_ctx* ctx, int enabled);
+int xfg_stage_times(const xfg_ctx* ctx, double* ms, const char** names, int max);
+/* times `iters` launches of the trace LDE kernels (7 columns x count proofs, resident device
+ * buffers, HIP events on the context stream); returns average ms per launch set in *avg_ms */
+int xfg_bench_lde(xfg_ctx* ctx, uint32_t count, uint64_t n, uint32_t blowup, uint32_t iters, double* avg_ms);
+/* kernel-level parity hooks (host buffers in/out) */
+int xfg_debug_lde(xfg_ctx* ctx, const uint64_t* coef, uint32_t npoly, uint64_t n, uint32_t blowup, uint64_t* out);
+int xfg_debug_interpolate(xfg_ctx* ctx, const uint64_t* evals, uint32_t npoly, uint64_t n, int offset7,
+                          uint64_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

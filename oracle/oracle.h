@@ -88,6 +88,8 @@ void orc_build_trace(const orc_air* air, uint64_t n, uint64_t* trace);
  * proof bytes are identical either way. out == NULL -> *out_len = required size. */
 int orc_prove(const orc_air* air, const uint64_t* trace, uint64_t n, const orc_options* opt, int faithful,
               uint8_t* out, size_t* out_len, orc_debug* dbg);
+/* evaluate_transition on one frame (src/burn_mint_air.rs:335-378) */
+void orc_eval_transition(const orc_air* air, const uint64_t cur[7], const uint64_t nxt[7], uint64_t r[7]);
 /* upper bound on proof size for buffer allocation */
 size_t orc_proof_size_bound(uint64_t n, const orc_options* opt);
 /* verifier restatement (Winterfell 0.8 verify) used as the oracle's self-check */

@@ -290,6 +290,9 @@ static void air_transition(const orc_air* air, const uint64_t cur[7], const uint
     r[5] = orc_sub(cur[5], nullifier);
     r[6] = orc_sub(cur[6], commitment);
 }
+void orc_eval_transition(const orc_air* air, const uint64_t cur[7], const uint64_t nxt[7], uint64_t r[7]) {
+    air_transition(air, cur, nxt, 0, r);
+}
 /* src/burn_mint_air.rs:380-395 get_assertions: 8 single assertions, final step n-1 (A.3);
  * already in Winterfell's (stride, first_step, column) order. */
 static void air_assertions(const orc_air* air, uint64_t n, uint64_t col[8], uint64_t step[8], uint64_t val[8]) {

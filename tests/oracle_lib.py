@@ -62,6 +62,7 @@ def lib():
         L.orc_proof_size_bound.restype = C.c_size_t
         L.orc_proof_size_bound.argtypes = [C.c_uint64, C.POINTER(Options)]
         L.orc_verify.argtypes = [C.POINTER(Air), C.c_char_p, C.c_size_t, C.POINTER(Options)]
+        L.orc_eval_transition.argtypes = [C.POINTER(Air), u64p, u64p, u64p]
         L.orc_interpolate.argtypes = [u64p, C.c_uint64, C.c_uint64]
         L.orc_evaluate_lde.argtypes = [u64p, C.c_uint64, C.c_uint64, C.c_uint64, u64p]
         _lib = L
@@ -121,3 +122,24 @@ def prove(air, n, opts, trace=None, faithful=False, debug=False):
 
 def verify(air, proof: bytes, opts) -> int:
     return lib().orc_verify(C.byref(air), proof, len(proof), C.byref(opts))
+
+
+def eval_transition(air, cur, nxt):
+    r = (C.c_uint64 * 7)()
+    lib().orc_eval_transition(C.byref(air), (C.c_uint64 * 7)(*cur), (C.c_uint64 * 7)(*nxt), r)
+    return list(r)
+
+
+def interpolate(vals, offset=1):
+    n = len(vals)
+    buf = (C.c_uint64 * n)(*vals)
+    lib().orc_interpolate(buf, n, offset)
+    return list(buf)
+
+
+def evaluate_lde(coef, blowup, offset=7):
+    n = len(coef)
+    cb = (C.c_uint64 * n)(*coef)
+    out = (C.c_uint64 * (n * blowup))()
+    lib().orc_evaluate_lde(cb, n, blowup, offset, out)
+    return list(out)

@@ -1,0 +1,174 @@
+"""GPU parity: libxfgstark.so (HIP, gfx950) against the CPU oracle, bit for bit.
+
+Kernel level: coset LDE / interpolation vs oracle NTT. Proof level: StarkProof bytes of the GPU
+path == oracle bytes on the same ExecutionTrace / burn inputs (small sizes run the oracle live;
+config-2 size n=2^16 is checked against the committed oracle fixture digest). Large sizes beyond
+the fixtures are checked through size-independent properties (the oracle verifier accepts,
+determinism, batch == single)."""
+import hashlib
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import synthetic
+
+pytestmark = pytest.mark.gpu
+P = 0xFFFFFFFF00000001
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def prover():
+    import xfgstark
+    pr = xfgstark.XfgBurnMintProver()
+    yield pr
+    pr.close()
+
+
+def oracle_air(kw):
+    st, air = O.air_from_inputs(kw["burn_amount"], kw["mint_amount"], kw["tx_prefix_hash"], kw["recipient_address"],
+                                kw["secret"], kw["network_id"], kw["target_chain_id"], kw["commitment_version"])
+    assert st == 0
+    return air
+
+
+def with_blowup(prover, b):
+    import xfgstark
+    o = xfgstark.ProofOptions.reference()
+    o.blowup_factor = b
+    prover._options = o
+    return o
+
+
+@pytest.mark.parametrize("n,blowup", [(8, 2), (64, 8), (256, 16), (1024, 4), (4096, 8), (1 << 15, 8)])
+def test_lde_kernel_matches_oracle(prover, n, blowup):
+    rng = np.random.default_rng(n + blowup)
+    coef = rng.integers(0, P, size=(3, n), dtype=np.uint64)
+    got = prover.debug_lde(coef, n, blowup)
+    for p in range(3):
+        want = O.evaluate_lde([int(v) for v in coef[p]], blowup, 7)
+        assert [int(v) for v in got[p]] == want
+
+
+@pytest.mark.parametrize("n,off7", [(8, False), (64, True), (2048, False), (2048, True), (1 << 14, True)])
+def test_interpolate_kernel_matches_oracle(prover, n, off7):
+    rng = np.random.default_rng(n)
+    ev = rng.integers(0, P, size=(2, n), dtype=np.uint64)
+    got = prover.debug_interpolate(ev, n, off7)
+    for p in range(2):
+        want = O.interpolate([int(v) for v in ev[p]], 7 if off7 else 1)
+        assert [int(v) for v in got[p]] == want
+
+
+@pytest.mark.parametrize("src,n,blowup", [("package", 64, 8), ("package", 64, 4), (0, 8, 8), (1, 16, 4), (7, 32, 2),
+                                          (2, 128, 8), (3, 1024, 4), (4, 1024, 8), (5, 2048, 16), (6, 4096, 8)])
+def test_prove_trace_bytes_match_oracle(prover, src, n, blowup):
+    kw = synthetic.REFERENCE_PACKAGE if src == "package" else synthetic.burn_inputs(src)
+    air = oracle_air(kw)
+    opts = O.options(blowup=blowup)
+    st, want = O.prove(air, n, opts)
+    assert st == 0
+    with_blowup(prover, blowup)
+    trace = np.frombuffer(bytes(O.build_trace(air, n)), dtype=np.uint64).reshape(7, n)
+    got = prover.prove_trace(trace, list(air.pub), air.nullifier, air.commitment).to_bytes()
+    assert got == want
+    assert O.verify(air, got, opts) == 0
+
+
+@pytest.mark.parametrize("case", json.load(open(os.path.join(GOLD, "proofs.json"))), ids=lambda c: c["name"])
+def test_prove_burn_mint_matches_golden(prover, case):
+    kw = synthetic.REFERENCE_PACKAGE if case["source"] == "package" else synthetic.burn_inputs(case["source"])
+    with_blowup(prover, case["blowup"])
+    proof = prover.prove_burn_mint(**kw, trace_length=case["n"]).to_bytes()
+    assert len(proof) == case["len"]
+    assert hashlib.sha256(proof).hexdigest() == case["sha256"]
+    if "proof_hex" in case:
+        assert proof.hex() == case["proof_hex"]
+
+
+def test_batch_equals_oracle_per_proof(prover):
+    with_blowup(prover, 8)
+    n = 1024
+    inputs = [synthetic.burn_inputs(100 + i) for i in range(6)]
+    proofs = prover.prove_batch(inputs, trace_length=n)
+    for kw, pr in zip(inputs, proofs):
+        st, want = O.prove(oracle_air(kw), n, O.options())
+        assert pr.to_bytes() == want
+
+
+def test_batch_isolates_invalid_inputs(prover):
+    import xfgstark
+    with_blowup(prover, 8)
+    good = synthetic.burn_inputs(7)
+    bad_burn = dict(good, burn_amount=1000, mint_amount=1000)
+    bad_tx = dict(good, tx_prefix_hash=bytes(32))
+    bad_rcpt = dict(good, recipient_address=b"\x01" * 19)
+    res = prover.prove_batch([bad_burn, good, bad_tx, bad_rcpt, good], trace_length=256)
+    assert isinstance(res[0], xfgstark.XfgStarkError) and res[0].status == 1
+    assert isinstance(res[2], xfgstark.XfgStarkError) and res[2].status == 3
+    assert isinstance(res[3], xfgstark.XfgStarkError) and res[3].status == 4
+    st, want = O.prove(oracle_air(good), 256, O.options())
+    assert res[1].to_bytes() == want == res[4].to_bytes()
+
+
+def test_prove_burn_mint_errors_carry_reference_messages(prover):
+    import xfgstark
+    kw = synthetic.burn_inputs(1)
+    with pytest.raises(xfgstark.XfgStarkError) as e:
+        prover.prove_burn_mint(**dict(kw, mint_amount=16_000_000))
+    assert "does not match burn amount" in str(e.value) and e.value.status == 2
+    with pytest.raises(xfgstark.XfgStarkError) as e:
+        prover.prove_burn_mint(**dict(kw, burn_amount=5))
+    assert str(e.value).startswith("Burn amount must be exactly 0.8 XFG")
+
+
+def test_invalid_trace_same_outcome_as_oracle(prover):
+    import xfgstark
+    kw = synthetic.burn_inputs(12)
+    air = oracle_air(kw)
+    n = 512
+    tr = O.build_trace(air, n)
+    tr[4 * n + 100] = 2  # illegal state jump
+    opts = O.options()
+    st, want = O.prove(air, n, opts, trace=tr)
+    with_blowup(prover, 8)
+    trace = np.frombuffer(bytes(tr), dtype=np.uint64).reshape(7, n)
+    if st == 0:
+        got = prover.prove_trace(trace, list(air.pub), air.nullifier, air.commitment).to_bytes()
+        assert got == want
+        assert O.verify(air, got, opts) != 0
+    else:
+        with pytest.raises(xfgstark.XfgStarkError):
+            prover.prove_trace(trace, list(air.pub), air.nullifier, air.commitment)
+
+
+@pytest.mark.parametrize("logn,blowup", [(17, 8), (18, 8), (20, 16)])
+def test_large_traces_verify(prover, logn, blowup):
+    # beyond fixture sizes: the oracle verifier (fast, O(queries * log N)) must accept the GPU proof,
+    # and proving twice is deterministic
+    kw = synthetic.burn_inputs(logn)
+    with_blowup(prover, blowup)
+    n = 1 << logn
+    p1 = prover.prove_burn_mint(**kw, trace_length=n).to_bytes()
+    p2 = prover.prove_burn_mint(**kw, trace_length=n).to_bytes()
+    assert p1 == p2
+    assert O.verify(oracle_air(kw), p1, O.options(blowup=blowup)) == 0
+
+
+def test_rejects_options_the_reference_rejects(prover):
+    import xfgstark
+    kw = synthetic.burn_inputs(3)
+    with_blowup(prover, 2)
+    with pytest.raises(xfgstark.XfgStarkError) as e:  # 42 queries >= LDE domain of 32
+        prover.prove_burn_mint(**kw, trace_length=16)
+    assert e.value.status == 6
+    with_blowup(prover, 3)
+    with pytest.raises(xfgstark.XfgStarkError):
+        prover.prove_burn_mint(**kw, trace_length=64)
+    with_blowup(prover, 8)
+    with pytest.raises(xfgstark.XfgStarkError):
+        prover.prove_burn_mint(**kw, trace_length=100)

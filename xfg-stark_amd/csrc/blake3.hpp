@@ -1,0 +1,112 @@
+// BLAKE3 compression for the Merkle commitments and Fiat-Shamir transcript of the burn-proof
+// STARK (winter-crypto `Blake3_256`, reference src/burn_mint_air.rs:483-485).
+// Everything on the hot path is a single 64-byte-or-shorter block: leaf = one trace row
+// (7 elements = 56 B), FRI leaf = 8 elements (64 B), Merkle node = two digests (64 B),
+// coin step = digest||u64 (40 B). Digests are 8 little-endian u32 words, so field elements map
+// to message words directly (lo, hi) -- no byte shuffling on the GPU.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace xfg {
+
+struct Digest {
+    uint32_t w[8];
+};
+
+#define XFG_B3_IV0 0x6A09E667u
+#define XFG_B3_IV1 0xBB67AE85u
+#define XFG_B3_IV2 0x3C6EF372u
+#define XFG_B3_IV3 0xA54FF53Au
+#define XFG_B3_IV4 0x510E527Fu
+#define XFG_B3_IV5 0x9B05688Cu
+#define XFG_B3_IV6 0x1F83D9ABu
+#define XFG_B3_IV7 0x5BE0CD19u
+
+enum : uint32_t { B3_CHUNK_START = 1, B3_CHUNK_END = 2, B3_PARENT = 4, B3_ROOT = 8 };
+
+__host__ __device__ __forceinline__ uint32_t b3_rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+
+#define XFG_B3_G(a, b, c, d, x, y)            \
+    do {                                      \
+        s[a] = s[a] + s[b] + (x);             \
+        s[d] = b3_rotr(s[d] ^ s[a], 16);      \
+        s[c] = s[c] + s[d];                   \
+        s[b] = b3_rotr(s[b] ^ s[c], 12);      \
+        s[a] = s[a] + s[b] + (y);             \
+        s[d] = b3_rotr(s[d] ^ s[a], 8);       \
+        s[c] = s[c] + s[d];                   \
+        s[b] = b3_rotr(s[b] ^ s[c], 7);       \
+    } while (0)
+
+// one round with message words already permuted into m[]
+#define XFG_B3_ROUND(m)                                   \
+    do {                                                  \
+        XFG_B3_G(0, 4, 8, 12, m[0], m[1]);                \
+        XFG_B3_G(1, 5, 9, 13, m[2], m[3]);                \
+        XFG_B3_G(2, 6, 10, 14, m[4], m[5]);               \
+        XFG_B3_G(3, 7, 11, 15, m[6], m[7]);               \
+        XFG_B3_G(0, 5, 10, 15, m[8], m[9]);               \
+        XFG_B3_G(1, 6, 11, 12, m[10], m[11]);             \
+        XFG_B3_G(2, 7, 8, 13, m[12], m[13]);              \
+        XFG_B3_G(3, 4, 9, 14, m[14], m[15]);              \
+    } while (0)
+
+// BLAKE3 message permutation applied in registers between rounds (compile-time indices)
+#define XFG_B3_PERMUTE(m)                                                                   \
+    do {                                                                                    \
+        uint32_t t0 = m[0], t1 = m[1], t2 = m[2], t3 = m[3], t4 = m[4], t5 = m[5], t6 = m[6], \
+                 t7 = m[7], t8 = m[8], t9 = m[9], t10 = m[10], t11 = m[11], t12 = m[12],      \
+                 t13 = m[13], t14 = m[14], t15 = m[15];                                     \
+        m[0] = t2; m[1] = t6; m[2] = t3; m[3] = t10; m[4] = t7; m[5] = t0; m[6] = t4;        \
+        m[7] = t13; m[8] = t1; m[9] = t11; m[10] = t12; m[11] = t5; m[12] = t9; m[13] = t14; \
+        m[14] = t15; m[15] = t8;                                                            \
+    } while (0)
+
+// compression returning the first 8 output words (chaining value / digest)
+__host__ __device__ __forceinline__ void b3_compress(const uint32_t cv[8], uint32_t m[16], uint32_t block_len,
+                                                     uint64_t counter, uint32_t flags, uint32_t out[8]) {
+    uint32_t s[16] = {cv[0], cv[1], cv[2], cv[3], cv[4], cv[5], cv[6], cv[7],
+                      XFG_B3_IV0, XFG_B3_IV1, XFG_B3_IV2, XFG_B3_IV3,
+                      (uint32_t)counter, (uint32_t)(counter >> 32), block_len, flags};
+    XFG_B3_ROUND(m); XFG_B3_PERMUTE(m);
+    XFG_B3_ROUND(m); XFG_B3_PERMUTE(m);
+    XFG_B3_ROUND(m); XFG_B3_PERMUTE(m);
+    XFG_B3_ROUND(m); XFG_B3_PERMUTE(m);
+    XFG_B3_ROUND(m); XFG_B3_PERMUTE(m);
+    XFG_B3_ROUND(m); XFG_B3_PERMUTE(m);
+    XFG_B3_ROUND(m);
+#pragma unroll
+    for (int i = 0; i < 8; i++) out[i] = s[i] ^ s[i + 8];
+}
+
+// BLAKE3 of a single block of `len` (<= 64) bytes given as 16 LE words (zero padded)
+__host__ __device__ __forceinline__ Digest b3_hash_block(uint32_t m[16], uint32_t len) {
+    const uint32_t iv[8] = {XFG_B3_IV0, XFG_B3_IV1, XFG_B3_IV2, XFG_B3_IV3,
+                            XFG_B3_IV4, XFG_B3_IV5, XFG_B3_IV6, XFG_B3_IV7};
+    Digest d;
+    b3_compress(iv, m, len, 0, B3_CHUNK_START | B3_CHUNK_END | B3_ROOT, d.w);
+    return d;
+}
+// Blake3_256::merge([a, b]) = BLAKE3(a || b)
+__host__ __device__ __forceinline__ Digest b3_merge(const Digest& a, const Digest& b) {
+    uint32_t m[16];
+#pragma unroll
+    for (int i = 0; i < 8; i++) { m[i] = a.w[i]; m[8 + i] = b.w[i]; }
+    return b3_hash_block(m, 64);
+}
+// Blake3_256::hash_elements for up to 8 field elements (one block)
+template <int K>
+__host__ __device__ __forceinline__ Digest b3_hash_elems(const uint64_t* e) {
+    static_assert(K >= 1 && K <= 8, "single-block element hash");
+    uint32_t m[16];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        uint64_t v = i < K ? e[i] : 0;
+        m[2 * i] = (uint32_t)v;
+        m[2 * i + 1] = (uint32_t)(v >> 32);
+    }
+    return b3_hash_block(m, 8 * K);
+}
+
+}  // namespace xfg

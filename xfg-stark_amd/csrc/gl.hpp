@@ -1,0 +1,62 @@
+// Goldilocks field p = 2^64 - 2^32 + 1 for CDNA4 (gfx950) kernels and the host orchestration.
+// Same field as Winterfell `math::fields::f64::BaseElement` used by the reference AIR
+// (reference src/burn_mint_air.rs:17). All values held in HBM are canonical (< p), so the proof
+// bytes are simply little-endian u64 words.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace xfg {
+
+typedef uint64_t u64;
+typedef uint32_t u32;
+
+constexpr u64 P = 0xFFFFFFFF00000001ULL;
+constexpr u64 EPS = 0xFFFFFFFFULL;  // 2^64 mod p
+constexpr u64 GEN = 7;              // multiplicative generator == Winterfell domain offset
+constexpr u64 TWO_ADIC_ROOT = 1753635133440165772ULL;  // 7^((p-1)/2^32)
+
+__host__ __device__ __forceinline__ u64 gl_add(u64 a, u64 b) {
+    u64 s = a + b;
+    s = (s < a) ? s + EPS : s;  // wrapped: +2^64 == +EPS (cannot wrap again for a,b < p)
+    return (s >= P) ? s - P : s;
+}
+__host__ __device__ __forceinline__ u64 gl_sub(u64 a, u64 b) {
+    u64 d = a - b;
+    return (a < b) ? d - EPS : d;  // borrowed: -2^64 == -EPS
+}
+__host__ __device__ __forceinline__ u64 gl_neg(u64 a) { return a ? P - a : 0; }
+
+__host__ __device__ __forceinline__ u64 mulhi64(u64 a, u64 b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __umul64hi(a, b);
+#else
+    return (u64)(((unsigned __int128)a * b) >> 64);
+#endif
+}
+// reduce hi*2^64 + lo using 2^64 == 2^32 - 1 and 2^96 == -1
+__host__ __device__ __forceinline__ u64 gl_reduce(u64 hi, u64 lo) {
+    u64 hh = hi >> 32, hl = hi & EPS;
+    u64 t0 = lo - hh;
+    t0 = (lo < hh) ? t0 - EPS : t0;
+    u64 t1 = hl * EPS;  // (hl << 32) - hl
+    u64 t2 = t0 + t1;
+    t2 = (t2 < t1) ? t2 + EPS : t2;
+    return (t2 >= P) ? t2 - P : t2;
+}
+__host__ __device__ __forceinline__ u64 gl_mul(u64 a, u64 b) { return gl_reduce(mulhi64(a, b), a * b); }
+__host__ __device__ __forceinline__ u64 gl_sqr(u64 a) { return gl_mul(a, a); }
+__host__ __device__ inline u64 gl_pow(u64 b, u64 e) {
+    u64 r = 1;
+    while (e) {
+        if (e & 1) r = gl_mul(r, b);
+        b = gl_mul(b, b);
+        e >>= 1;
+    }
+    return r;
+}
+__host__ __device__ inline u64 gl_inv(u64 a) { return gl_pow(a, P - 2); }
+// winter-math get_root_of_unity(k): primitive 2^k-th root
+__host__ __device__ inline u64 gl_root(unsigned k) { return gl_pow(TWO_ADIC_ROOT, 1ULL << (32 - k)); }
+
+}  // namespace xfg

@@ -1,0 +1,706 @@
+// HIP kernels (CDNA4 / gfx950) for the XFG burn-proof STARK hot path.
+//
+// Replaces, inside Winterfell 0.8.3 `Prover::prove` as bound by the reference
+// (src/burn_mint_air.rs:479-531, called at src/burn_mint_prover.rs:124-126):
+//   - DefaultTraceLde: column interpolation + coset LDE (four-step NTT, LDS radix-2 stages)
+//   - RowMatrix::commit_to_rows / MerkleTree::new: Blake3 row hashing + binary Merkle tree
+//   - DefaultConstraintEvaluator with XfgBurnMintAir::evaluate_transition (:335-378) and the
+//     8 assertions (:380-395), batch-inverted divisors
+//   - CompositionPoly / DeepCompositionPoly: OOD evaluation, coefficient-domain DEEP combine with
+//     synthetic division expressed as a weighted suffix scan
+//   - FriProver::build_layers: fold-by-8 (apply_drp) and per-layer commitments
+// All arithmetic is 64-bit Goldilocks integer work: HBM/VALU bound, no MFMA.
+#include "kernels.hpp"
+
+namespace xfg {
+
+#define XFG_CHECK_LAUNCH() (void)hipGetLastError()
+
+__device__ __forceinline__ unsigned brev(unsigned x, int bits) { return __brev(x) >> (32 - bits); }
+
+// w_{2^k}^e from the master table (forward) / its inverse
+__device__ __forceinline__ u64 tw_pow(const Tables& T, int k, u64 e) {
+    u64 M = 1ULL << T.LM;
+    return T.tw[(e << (T.LM - k)) & (M - 1)];
+}
+__device__ __forceinline__ u64 tw_ipow(const Tables& T, int k, u64 e) {
+    u64 M = 1ULL << T.LM;
+    return T.tw[(M - ((e << (T.LM - k)) & (M - 1))) & (M - 1)];
+}
+
+// ============================================================================ NTT
+struct NttArgs {
+    const u64* in;
+    u64* y;
+    u64* out;
+    u64 in_stride, out_stride;
+    int logn, logR, logC, logTC, logTR;
+    int logbeta;  // forward: number of cosets = 2^logbeta
+    int inverse;
+    int off7;
+    u64 scale;
+    u64 keep;
+    Tables T;
+};
+
+// radix-2 DIT stages over `nseq` sequences of length 2^logS stored as rows of `tile` (row pitch
+// S+1, inputs already in bit-reversed positions); ltw[i] = w_S^{+-i}, i < S/2
+__device__ __forceinline__ void lds_dit(u64* tile, const u64* ltw, int logS, int nseq) {
+    const int S = 1 << logS, pitch = S + 1, half = S >> 1;
+    const int nb = nseq * half;
+    for (int s = 0; s < logS; s++) {
+        const int h = 1 << s;
+        for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+            int seq = b >> (logS - 1), bi = b & (half - 1);
+            int pos = bi & (h - 1), i0 = ((bi >> s) << (s + 1)) + pos;
+            u64* row = tile + seq * pitch;
+            u64 w = ltw[pos << (logS - 1 - s)];
+            u64 u = row[i0], v = gl_mul(row[i0 + h], w);
+            row[i0] = gl_add(u, v);
+            row[i0 + h] = gl_sub(u, v);
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void ntt_cols_kernel(NttArgs a) {
+    extern __shared__ u64 lds[];
+    const int R = 1 << a.logR, TC = 1 << a.logTC;
+    const u64 n = 1ULL << a.logn;
+    const int poly = blockIdx.y, col0 = blockIdx.x * TC;
+    u64* tile = lds;
+    u64* ltw = lds + TC * (R + 1);
+    for (int i = threadIdx.x; i < R / 2; i += blockDim.x)
+        ltw[i] = a.inverse ? tw_ipow(a.T, a.logR, i) : tw_pow(a.T, a.logR, i);
+    const int nelem = R * TC;
+    const u64* in = a.in + (u64)poly * a.in_stride;
+    const int ncos = a.inverse ? 1 : (1 << a.logbeta);
+    const int logN = a.logn + a.logbeta;
+    for (int t = 0; t < ncos; t++) {
+        for (int e = threadIdx.x; e < nelem; e += blockDim.x) {
+            int j1 = e >> a.logTC, jj = e & (TC - 1);
+            u64 j = ((u64)j1 << a.logC) + col0 + jj;
+            u64 v = in[j];
+            if (!a.inverse) {
+                // coset shift (7 w_N^t)^j folded into the load
+                v = gl_mul(v, a.T.pow7[j]);
+                if (t) v = gl_mul(v, tw_pow(a.T, logN, ((u64)t * j) & ((1ULL << logN) - 1)));
+            }
+            tile[jj * (R + 1) + brev(j1, a.logR)] = v;
+        }
+        __syncthreads();
+        lds_dit(tile, ltw, a.logR, TC);
+        u64* y = a.y + ((u64)poly * ncos + t) * n;
+        for (int e = threadIdx.x; e < nelem; e += blockDim.x) {
+            int k1 = e >> a.logTC, jj = e & (TC - 1);
+            u64 j2 = col0 + jj;
+            u64 ex = (j2 * (u64)k1) & (n - 1);
+            u64 w = a.inverse ? tw_ipow(a.T, a.logn, ex) : tw_pow(a.T, a.logn, ex);
+            y[((u64)k1 << a.logC) + j2] = gl_mul(tile[jj * (R + 1) + k1], w);
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void ntt_rows_kernel(NttArgs a) {
+    extern __shared__ u64 lds[];
+    const int C = 1 << a.logC, TR = 1 << a.logTR;
+    const u64 n = 1ULL << a.logn;
+    const int pt = blockIdx.y, k10 = blockIdx.x * TR;
+    u64* tile = lds;
+    u64* ltw = lds + TR * (C + 1);
+    for (int i = threadIdx.x; i < C / 2; i += blockDim.x)
+        ltw[i] = a.inverse ? tw_ipow(a.T, a.logC, i) : tw_pow(a.T, a.logC, i);
+    const int nelem = TR * C;
+    const u64* y = a.y + (u64)pt * n;
+    for (int e = threadIdx.x; e < nelem; e += blockDim.x) {
+        int r = e >> a.logC, j2 = e & (C - 1);
+        tile[r * (C + 1) + brev(j2, a.logC)] = y[((u64)(k10 + r) << a.logC) + j2];
+    }
+    __syncthreads();
+    lds_dit(tile, ltw, a.logC, TR);
+    for (int e = threadIdx.x; e < nelem; e += blockDim.x) {
+        int k2 = e >> a.logTR, r = e & (TR - 1);
+        u64 k = (u64)(k10 + r) + ((u64)k2 << a.logR);
+        u64 v = tile[r * (C + 1) + k2];
+        if (a.inverse) {
+            if (k >= a.keep) continue;
+            v = gl_mul(v, a.scale);
+            if (a.off7) v = gl_mul(v, a.T.ipow7[k]);
+            a.out[(u64)pt * a.out_stride + k] = v;
+        } else {
+            a.out[(u64)pt * n + k] = v;  // pt = poly * beta + t  -> coset-major
+        }
+    }
+}
+
+static void ntt_plan(NttArgs& a, int logn) {
+    a.logn = logn;
+    a.logR = logn / 2;
+    a.logC = logn - a.logR;
+    a.logTC = a.logC < 12 - a.logR ? a.logC : 12 - a.logR;
+    a.logTR = a.logR < 12 - a.logC ? a.logR : 12 - a.logC;
+    if (a.logTC < 0) a.logTC = 0;
+    if (a.logTR < 0) a.logTR = 0;
+}
+static void ntt_run(NttArgs& a, int npoly, int ncos, hipStream_t s) {
+    const int R = 1 << a.logR, C = 1 << a.logC;
+    size_t lds1 = ((size_t)(1 << a.logTC) * (R + 1) + R / 2) * sizeof(u64);
+    size_t lds2 = ((size_t)(1 << a.logTR) * (C + 1) + C / 2) * sizeof(u64);
+    dim3 g1(C >> a.logTC, npoly), g2(R >> a.logTR, npoly * ncos);
+    hipLaunchKernelGGL(ntt_cols_kernel, g1, dim3(256), lds1, s, a);
+    hipLaunchKernelGGL(ntt_rows_kernel, g2, dim3(256), lds2, s, a);
+    XFG_CHECK_LAUNCH();
+}
+
+void launch_lde(const u64* coef, u64 coef_stride, u64* out, u64* scratch, int npoly, int logn, int logbeta,
+                const Tables& T, hipStream_t s) {
+    NttArgs a{};
+    ntt_plan(a, logn);
+    a.in = coef; a.in_stride = coef_stride; a.y = scratch; a.out = out;
+    a.logbeta = logbeta; a.inverse = 0; a.T = T;
+    ntt_run(a, npoly, 1 << logbeta, s);
+}
+void launch_interpolate(const u64* evals, u64 in_stride, u64* out, u64 out_stride, u64* scratch, int npoly, int logn,
+                        bool off7, u64 keep, const Tables& T, hipStream_t s) {
+    NttArgs a{};
+    ntt_plan(a, logn);
+    a.in = evals; a.in_stride = in_stride; a.y = scratch; a.out = out; a.out_stride = out_stride;
+    a.logbeta = 0; a.inverse = 1; a.off7 = off7 ? 1 : 0; a.keep = keep; a.T = T;
+    a.scale = gl_inv(1ULL << logn);
+    ntt_run(a, npoly, 1, s);
+}
+
+// ============================================================================ Merkle
+// builds `levels` levels above the per-thread nodes held in lds[0..nthreads) and writes them;
+// node index of thread i at the base level is base_idx + i
+__device__ __forceinline__ void lds_subtree(Digest* lds, Digest mine, Digest* nodes, u64 base_idx, int levels) {
+    const int tid = threadIdx.x;
+    lds[tid] = mine;
+    __syncthreads();
+    for (int l = 1; l <= levels; l++) {
+        int cnt = blockDim.x >> l;
+        Digest d;
+        if (tid < cnt) d = b3_merge(lds[2 * tid], lds[2 * tid + 1]);
+        __syncthreads();
+        if (tid < cnt) {
+            lds[tid] = d;
+            nodes[(base_idx >> l) + tid] = d;
+        }
+        __syncthreads();
+    }
+}
+
+// subtree over leaves t = T0 .. T0 + 2^LOG - 1 of LDE row m (leaf k = (m << LOGB) + t); compile-time
+// recursion keeps every intermediate digest in registers
+template <int NC, int LOGB, int LOG, int T0>
+__device__ __forceinline__ Digest lde_subtree(const u64* base, u64 n, u64 m, Digest* nodes, u64 L) {
+    if constexpr (LOG == 0) {
+        u64 row[NC];
+#pragma unroll
+        for (int c = 0; c < NC; c++) row[c] = base[((u64)c * (1 << LOGB) + T0) * n + m];
+        Digest d = b3_hash_elems<NC>(row);
+        nodes[L + (m << LOGB) + T0] = d;
+        return d;
+    } else {
+        Digest l = lde_subtree<NC, LOGB, LOG - 1, T0>(base, n, m, nodes, L);
+        Digest r = lde_subtree<NC, LOGB, LOG - 1, T0 + (1 << (LOG - 1))>(base, n, m, nodes, L);
+        Digest p = b3_merge(l, r);
+        nodes[(L + (m << LOGB) + T0) >> LOG] = p;
+        return p;
+    }
+}
+
+template <int NC, int LOGB>
+__global__ __launch_bounds__(256) void leaves_lde_kernel(const u64* lde, Digest* nodes_all, u64 node_stride,
+                                                         int logn) {
+    __shared__ Digest lds[256];
+    constexpr int B = 1 << LOGB;
+    const u64 n = 1ULL << logn, L = n << LOGB;
+    const int proof = blockIdx.y;
+    const u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x;  // grid covers n exactly
+    const u64* base = lde + (u64)proof * NC * B * n;
+    Digest* nodes = nodes_all + (u64)proof * node_stride;
+    Digest top = lde_subtree<NC, LOGB, LOGB, 0>(base, n, m, nodes, L);
+    int levels = 31 - __clz(blockDim.x);
+    lds_subtree(lds, top, nodes, n + (u64)blockIdx.x * blockDim.x, levels);
+}
+
+template <int NC>
+static void leaves_lde_dispatch(int logbeta, dim3 g, dim3 b, hipStream_t s, const u64* lde, Digest* nodes,
+                                u64 stride, int logn) {
+    switch (logbeta) {
+        case 1: hipLaunchKernelGGL((leaves_lde_kernel<NC, 1>), g, b, 0, s, lde, nodes, stride, logn); break;
+        case 2: hipLaunchKernelGGL((leaves_lde_kernel<NC, 2>), g, b, 0, s, lde, nodes, stride, logn); break;
+        case 3: hipLaunchKernelGGL((leaves_lde_kernel<NC, 3>), g, b, 0, s, lde, nodes, stride, logn); break;
+        case 4: hipLaunchKernelGGL((leaves_lde_kernel<NC, 4>), g, b, 0, s, lde, nodes, stride, logn); break;
+        default: break;
+    }
+}
+void launch_leaves_lde(const u64* lde, int nc, Digest* nodes, u64 node_stride, int npoly, int logn, int logbeta,
+                       hipStream_t s) {
+    u64 n = 1ULL << logn;
+    int threads = n < 256 ? (int)n : 256;
+    dim3 g((unsigned)(n / threads), npoly), b(threads);
+    if (nc == 7) leaves_lde_dispatch<7>(logbeta, g, b, s, lde, nodes, node_stride, logn);
+    else leaves_lde_dispatch<1>(logbeta, g, b, s, lde, nodes, node_stride, logn);
+    XFG_CHECK_LAUNCH();
+}
+
+__global__ __launch_bounds__(256) void tree_levels_kernel(Digest* nodes_all, u64 node_stride, u64 count, int levels) {
+    __shared__ Digest lds[256];
+    Digest* nodes = nodes_all + (u64)blockIdx.y * node_stride;
+    const u64 first = count + (u64)blockIdx.x * (2 * blockDim.x);
+    const int tid = threadIdx.x;
+    Digest d = b3_merge(nodes[first + 2 * tid], nodes[first + 2 * tid + 1]);
+    nodes[(first >> 1) + tid] = d;
+    lds_subtree(lds, d, nodes, first >> 1, levels - 1);
+}
+void launch_tree_top(Digest* nodes, u64 node_stride, u64 count, int npoly, hipStream_t s) {
+    while (count > 1) {
+        int lg = 0;
+        while ((1ULL << (lg + 1)) <= count) lg++;
+        int levels = lg < 9 ? lg : 9;
+        int threads = 1 << (levels - 1);
+        dim3 g((unsigned)(count >> levels), npoly);
+        hipLaunchKernelGGL(tree_levels_kernel, g, dim3(threads), 0, s, nodes, node_stride, count, levels);
+        count >>= levels;
+    }
+    XFG_CHECK_LAUNCH();
+}
+
+// FRI layer value at natural index K of a layer stored coset-major (layer 0) or natural
+__device__ __forceinline__ u64 layer_at(const u64* base, bool coset_major, int logn, int logbeta, u64 K) {
+    if (!coset_major) return base[K];
+    u64 t = K & ((1ULL << logbeta) - 1), m = K >> logbeta;
+    return base[(t << logn) + m];
+}
+
+__global__ __launch_bounds__(256) void fri_leaves_kernel(const u64* vals, u64 val_stride, int coset_major, int logn,
+                                                         int logbeta, u64 rows, Digest* nodes_all, u64 node_stride) {
+    __shared__ Digest lds[256];
+    const int proof = blockIdx.y;
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    const u64* base = vals + (u64)proof * val_stride;
+    Digest* nodes = nodes_all + (u64)proof * node_stride;
+    u64 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[k] = layer_at(base, coset_major, logn, logbeta, i + (u64)k * rows);
+    Digest d = b3_hash_elems<8>(v);
+    nodes[rows + i] = d;
+    int levels = 31 - __clz(blockDim.x);
+    lds_subtree(lds, d, nodes, rows + (u64)blockIdx.x * blockDim.x, levels);
+}
+void launch_fri_leaves(const u64* vals, u64 val_stride, bool coset_major, int logn, int logbeta, u64 rows,
+                       Digest* nodes, u64 node_stride, int npoly, hipStream_t s) {
+    int threads = rows < 256 ? (int)rows : 256;
+    dim3 g((unsigned)(rows / threads), npoly);
+    hipLaunchKernelGGL(fri_leaves_kernel, g, dim3(threads), 0, s, vals, val_stride, coset_major ? 1 : 0, logn,
+                       logbeta, rows, nodes, node_stride);
+    XFG_CHECK_LAUNCH();
+}
+
+// ============================================================================ AIR
+__global__ void trace_gen_kernel(const AirConst* air, u64* trace, int logn) {
+    const u64 n = 1ULL << logn;
+    const u64 s = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    const int proof = blockIdx.y;
+    if (s >= n) return;
+    const AirConst& A = air[proof];
+    u64* tr = trace + (u64)proof * 7 * n;
+    // src/burn_mint_air.rs:442-476, state column = floor(4 step / n)
+    tr[0 * n + s] = A.pub[0];
+    tr[1 * n + s] = A.pub[1];
+    tr[2 * n + s] = A.pub[2];
+    tr[3 * n + s] = A.pub[3];
+    tr[4 * n + s] = (4 * s) >> logn;
+    tr[5 * n + s] = A.nullifier;
+    tr[6 * n + s] = A.commitment;
+}
+void launch_trace_gen(const AirConst* air, u64* trace, int logn, int npoly, hipStream_t s) {
+    u64 n = 1ULL << logn;
+    dim3 g((unsigned)((n + 255) / 256), npoly);
+    hipLaunchKernelGGL(trace_gen_kernel, g, dim3(256), 0, s, air, trace, logn);
+    XFG_CHECK_LAUNCH();
+}
+
+// Block-wide batch inversion (Montgomery trick), one value per thread, 256 threads.
+__device__ u64 block_batch_inverse(u64 v, u64* sh /* 2*256 */) {
+    const int tid = threadIdx.x, T = blockDim.x;
+    u64* pre = sh;
+    u64* suf = sh + 256;
+    pre[tid] = v;
+    suf[tid] = v;
+    __syncthreads();
+    // inclusive prefix / suffix products (Hillis-Steele)
+    for (int off = 1; off < T; off <<= 1) {
+        u64 a = pre[tid], b = suf[tid];
+        if (tid >= off) a = gl_mul(a, pre[tid - off]);
+        if (tid + off < T) b = gl_mul(b, suf[tid + off]);
+        __syncthreads();
+        pre[tid] = a;
+        suf[tid] = b;
+        __syncthreads();
+    }
+    u64 total = pre[T - 1];
+    __shared__ u64 inv_total;
+    if (tid == 0) inv_total = gl_inv(total);
+    __syncthreads();
+    u64 r = inv_total;
+    if (tid > 0) r = gl_mul(r, pre[tid - 1]);
+    if (tid + 1 < T) r = gl_mul(r, suf[tid + 1]);
+    __syncthreads();
+    return r;
+}
+
+struct CeArgs {
+    const u64* lde;
+    const AirConst* air;
+    const u64* coeffs;
+    u64* ce;
+    int logn, logbeta;
+    u64 g_last;          // g^(n-1)
+    u64 inv_xn1[2];      // 1/(x^n - 1) for even / odd CE index (x^n = +-7^n)
+    Tables T;
+};
+__global__ __launch_bounds__(256) void constraint_eval_kernel(CeArgs a) {
+    __shared__ u64 sh[512];
+    const u64 n = 1ULL << a.logn, nce = 2 * n;
+    const int proof = blockIdx.y;
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;  // grid covers nce exactly
+    const AirConst& A = a.air[proof];
+    const u64* co = a.coeffs + (u64)proof * 15;
+    const u64 beta = 1ULL << a.logbeta;
+    const u64* lde = a.lde + (u64)proof * 7 * beta * n;
+    // CE step i <-> LDE index i*beta/2 (ce_to_lde_blowup), coset-major (t, m)
+    const u64 t = (i & 1) ? beta / 2 : 0, m = i >> 1, mn = (m + 1) & (n - 1);
+    u64 cur[7];
+#pragma unroll
+    for (int c = 0; c < 7; c++) cur[c] = lde[(((u64)c << a.logbeta) + t) * n + m];
+    const u64 nxt4 = lde[((4ULL << a.logbeta) + t) * n + mn];
+    // XfgBurnMintAir::evaluate_transition (reference src/burn_mint_air.rs:335-378)
+    const u64 std_burn = 8000000ULL, large_burn = 8000000000ULL;
+    u64 r0 = gl_mul(gl_sub(cur[0], std_burn), gl_sub(cur[0], large_burn));
+    u64 r1 = gl_sub(cur[1], cur[0]);
+    u64 r2 = gl_sub(cur[2], A.pub[2] & 0xFFFFFFFFULL);
+    u64 r3 = gl_sub(cur[3], A.pub[3] & 0xFFFFFFFFULL);
+    u64 d = gl_sub(nxt4, cur[4]);
+    u64 r4 = gl_mul(d, gl_sub(d, 1));
+    u64 r5 = gl_sub(cur[5], A.nullifier);
+    u64 r6 = gl_sub(cur[6], A.commitment);
+    u64 tr = gl_mul(co[0], r0);
+    tr = gl_add(tr, gl_mul(co[1], r1));
+    tr = gl_add(tr, gl_mul(co[2], r2));
+    tr = gl_add(tr, gl_mul(co[3], r3));
+    tr = gl_add(tr, gl_mul(co[4], r4));
+    tr = gl_add(tr, gl_mul(co[5], r5));
+    tr = gl_add(tr, gl_mul(co[6], r6));
+    // assertions (src/burn_mint_air.rs:380-395): step 0 on columns 0..6, step n-1 on column 4
+    const u64 v0[7] = {A.pub[0], A.pub[1], A.pub[2], A.pub[3], 0, A.nullifier, A.commitment};
+    u64 b0 = 0;
+#pragma unroll
+    for (int c = 0; c < 7; c++) b0 = gl_add(b0, gl_mul(co[7 + c], gl_sub(cur[c], v0[c])));
+    u64 b1 = gl_mul(co[14], gl_sub(cur[4], 3));
+    // x = 7 w_2n^i ; divisors (x - 1), (x - g^(n-1)), (x^n - 1)
+    const u64 x = gl_mul(GEN, tw_pow(a.T, a.logn + 1, i));
+    const u64 xa = gl_sub(x, 1), xb = gl_sub(x, a.g_last);
+    u64 inv_ab = block_batch_inverse(gl_mul(xa, xb), sh);
+    u64 inv_a = gl_mul(inv_ab, xb), inv_b = gl_mul(inv_ab, xa);
+    u64 val = gl_mul(gl_mul(tr, xb), a.inv_xn1[i & 1]);
+    val = gl_add(val, gl_mul(b0, inv_a));
+    val = gl_add(val, gl_mul(b1, inv_b));
+    a.ce[(u64)proof * nce + i] = val;
+}
+void launch_constraint_eval(const u64* lde, const AirConst* air, const u64* coeffs, u64* ce, int logn, int logbeta,
+                            const Tables& T, int npoly, hipStream_t s) {
+    CeArgs a;
+    a.lde = lde; a.air = air; a.coeffs = coeffs; a.ce = ce; a.logn = logn; a.logbeta = logbeta; a.T = T;
+    u64 n = 1ULL << logn;
+    a.g_last = gl_pow(gl_root(logn), n - 1);
+    u64 sn = gl_pow(GEN, n);
+    a.inv_xn1[0] = gl_inv(gl_sub(sn, 1));
+    a.inv_xn1[1] = gl_inv(gl_sub(gl_neg(sn), 1));
+    u64 nce = 2 * n;
+    int threads = nce < 256 ? (int)nce : 256;
+    dim3 g((unsigned)(nce / threads), npoly);
+    hipLaunchKernelGGL(constraint_eval_kernel, g, dim3(threads), 0, s, a);
+    XFG_CHECK_LAUNCH();
+}
+
+// ============================================================================ OOD
+// partial sums of T_c(z), T_c(zg) (c < 7) and H(z); 8 consecutive coefficients per thread
+__global__ __launch_bounds__(256) void ood_partial_kernel(const u64* coef, const u64* hcoef, const u64* zpts,
+                                                          u64* partial, int logn) {
+    __shared__ u64 red[15][256];
+    const u64 n = 1ULL << logn;
+    const int proof = blockIdx.y, tid = threadIdx.x;
+    const u64 j0 = ((u64)blockIdx.x * blockDim.x + tid) * 8;
+    const u64 z = zpts[2 * proof], zg = zpts[2 * proof + 1];
+    u64 acc[15];
+#pragma unroll
+    for (int q = 0; q < 15; q++) acc[q] = 0;
+    if (j0 < n) {
+        u64 pz = gl_pow(z, j0), pzg = gl_pow(zg, j0);
+        const u64* co = coef + (u64)proof * 7 * n;
+        const u64* h = hcoef + (u64)proof * n;
+        const int cnt = n - j0 < 8 ? (int)(n - j0) : 8;
+        for (int r = 0; r < cnt; r++) {
+            u64 j = j0 + r;
+#pragma unroll
+            for (int c = 0; c < 7; c++) {
+                u64 v = co[(u64)c * n + j];
+                acc[2 * c] = gl_add(acc[2 * c], gl_mul(v, pz));
+                acc[2 * c + 1] = gl_add(acc[2 * c + 1], gl_mul(v, pzg));
+            }
+            acc[14] = gl_add(acc[14], gl_mul(h[j], pz));
+            pz = gl_mul(pz, z);
+            pzg = gl_mul(pzg, zg);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 15; q++) red[q][tid] = acc[q];
+    __syncthreads();
+    for (int off = blockDim.x / 2; off > 0; off >>= 1) {
+        if (tid < off) {
+#pragma unroll
+            for (int q = 0; q < 15; q++) red[q][tid] = gl_add(red[q][tid], red[q][tid + off]);
+        }
+        __syncthreads();
+    }
+    for (int q = tid; q < 15; q += blockDim.x) partial[((u64)proof * gridDim.x + blockIdx.x) * 15 + q] = red[q][0];
+}
+__global__ void ood_final_kernel(const u64* partial, int nblk, u64* ood) {
+    const int proof = blockIdx.x, q = threadIdx.x;
+    if (q >= 15) return;
+    u64 s = 0;
+    for (int b = 0; b < nblk; b++) s = gl_add(s, partial[((u64)proof * nblk + b) * 15 + q]);
+    ood[(u64)proof * 15 + q] = s;
+}
+void launch_ood(const u64* coef, const u64* hcoef, const u64* zpts, u64* partial, u64* ood, int logn, int npoly,
+                hipStream_t s) {
+    u64 n = 1ULL << logn;
+    u64 nthreads = (n + 7) / 8;
+    int threads = nthreads < 256 ? (int)nthreads : 256;
+    int nblk = (int)((nthreads + threads - 1) / threads);
+    hipLaunchKernelGGL(ood_partial_kernel, dim3(nblk, npoly), dim3(threads), 0, s, coef, hcoef, zpts, partial, logn);
+    hipLaunchKernelGGL(ood_final_kernel, dim3(npoly), dim3(64), 0, s, partial, nblk, ood);
+    XFG_CHECK_LAUNCH();
+}
+
+// ============================================================================ DEEP
+// P1_j = sum a_c T_c[j] + gamma H[j] - [j==0] c1 ; P2_j = sum a_c T_c[j] - [j==0] c2
+// quotient of P/(x - b): q_k = sum_{j>k} P_j b^(j-k-1) = b^-(k+1) * sum_{j>k} P_j b^j
+// s_j = P_j b^j (two streams) -> exclusive suffix sums -> d_k = z^-(k+1) E1_k + zg^-(k+1) E2_k
+#define DEEP_PER_THREAD 8
+__device__ __forceinline__ void deep_terms(const u64* co, const u64* h, const DeepParams& P, u64 n, u64 j, u64& p1,
+                                           u64& p2) {
+    u64 s = 0;
+#pragma unroll
+    for (int c = 0; c < 7; c++) s = gl_add(s, gl_mul(P.a[c], co[(u64)c * n + j]));
+    p1 = gl_add(s, gl_mul(P.gamma, h[j]));
+    p2 = s;
+    if (j == 0) {
+        p1 = gl_sub(p1, P.c1);
+        p2 = gl_sub(p2, P.c2);
+    }
+}
+__global__ __launch_bounds__(256) void deep_blocksum_kernel(const u64* coef, const u64* hcoef, const DeepParams* dp,
+                                                            u64* bsum, int logn) {
+    __shared__ u64 r1[256], r2[256];
+    const u64 n = 1ULL << logn;
+    const int proof = blockIdx.y, tid = threadIdx.x;
+    const DeepParams P = dp[proof];
+    const u64* co = coef + (u64)proof * 7 * n;
+    const u64* h = hcoef + (u64)proof * n;
+    const u64 j0 = ((u64)blockIdx.x * blockDim.x + tid) * DEEP_PER_THREAD;
+    u64 s1 = 0, s2 = 0;
+    if (j0 < n) {
+        u64 pz = gl_pow(P.z, j0), pzg = gl_pow(P.zg, j0);
+        for (int r = 0; r < DEEP_PER_THREAD && j0 + r < n; r++) {
+            u64 p1, p2;
+            deep_terms(co, h, P, n, j0 + r, p1, p2);
+            s1 = gl_add(s1, gl_mul(p1, pz));
+            s2 = gl_add(s2, gl_mul(p2, pzg));
+            pz = gl_mul(pz, P.z);
+            pzg = gl_mul(pzg, P.zg);
+        }
+    }
+    r1[tid] = s1;
+    r2[tid] = s2;
+    __syncthreads();
+    for (int off = blockDim.x / 2; off > 0; off >>= 1) {
+        if (tid < off) {
+            r1[tid] = gl_add(r1[tid], r1[tid + off]);
+            r2[tid] = gl_add(r2[tid], r2[tid + off]);
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        bsum[((u64)proof * gridDim.x + blockIdx.x) * 2] = r1[0];
+        bsum[((u64)proof * gridDim.x + blockIdx.x) * 2 + 1] = r2[0];
+    }
+}
+// exclusive suffix sums over blocks (serial per proof; nblk is small)
+__global__ void deep_carry_kernel(const u64* bsum, u64* carry, int nblk) {
+    const int proof = blockIdx.x, q = threadIdx.x;
+    if (q >= 2) return;
+    u64 s = 0;
+    for (int b = nblk - 1; b >= 0; b--) {
+        carry[((u64)proof * nblk + b) * 2 + q] = s;
+        s = gl_add(s, bsum[((u64)proof * nblk + b) * 2 + q]);
+    }
+}
+__global__ __launch_bounds__(256) void deep_final_kernel(const u64* coef, const u64* hcoef, const DeepParams* dp,
+                                                         const u64* carry, u64* deep, int logn) {
+    __shared__ u64 e1[256], e2[256];
+    const u64 n = 1ULL << logn;
+    const int proof = blockIdx.y, tid = threadIdx.x, T = blockDim.x;
+    const DeepParams P = dp[proof];
+    const u64* co = coef + (u64)proof * 7 * n;
+    const u64* h = hcoef + (u64)proof * n;
+    const u64 j0 = ((u64)blockIdx.x * T + tid) * DEEP_PER_THREAD;
+    u64 s1[DEEP_PER_THREAD], s2[DEEP_PER_THREAD];
+    u64 t1 = 0, t2 = 0;
+    {
+        u64 pz = j0 < n ? gl_pow(P.z, j0) : 0, pzg = j0 < n ? gl_pow(P.zg, j0) : 0;
+#pragma unroll
+        for (int r = 0; r < DEEP_PER_THREAD; r++) {
+            s1[r] = s2[r] = 0;
+            if (j0 + r < n) {
+                u64 p1, p2;
+                deep_terms(co, h, P, n, j0 + r, p1, p2);
+                s1[r] = gl_mul(p1, pz);
+                s2[r] = gl_mul(p2, pzg);
+                pz = gl_mul(pz, P.z);
+                pzg = gl_mul(pzg, P.zg);
+            }
+            t1 = gl_add(t1, s1[r]);
+            t2 = gl_add(t2, s2[r]);
+        }
+    }
+    // inclusive suffix scan of per-thread totals
+    e1[tid] = t1;
+    e2[tid] = t2;
+    __syncthreads();
+    for (int off = 1; off < T; off <<= 1) {
+        u64 a1 = e1[tid], a2 = e2[tid];
+        if (tid + off < T) {
+            a1 = gl_add(a1, e1[tid + off]);
+            a2 = gl_add(a2, e2[tid + off]);
+        }
+        __syncthreads();
+        e1[tid] = a1;
+        e2[tid] = a2;
+        __syncthreads();
+    }
+    // exclusive suffix (everything after this thread's chunk) + blocks after this one
+    u64 c1 = carry[((u64)proof * gridDim.x + blockIdx.x) * 2];
+    u64 c2 = carry[((u64)proof * gridDim.x + blockIdx.x) * 2 + 1];
+    u64 x1 = gl_add(c1, tid + 1 < T ? e1[tid + 1] : 0);
+    u64 x2 = gl_add(c2, tid + 1 < T ? e2[tid + 1] : 0);
+    if (j0 >= n) return;
+    // walk the chunk backwards: E_k = sum_{j>k} s_j
+    const int cnt = n - j0 < DEEP_PER_THREAD ? (int)(n - j0) : DEEP_PER_THREAD;
+    u64 last = j0 + cnt - 1;
+    u64 iz = gl_pow(P.zinv, last + 1), izg = gl_pow(P.zginv, last + 1);
+    u64* out = deep + (u64)proof * n;
+    for (int r = cnt - 1; r >= 0; r--) {
+        out[j0 + r] = gl_add(gl_mul(iz, x1), gl_mul(izg, x2));
+        x1 = gl_add(x1, s1[r]);
+        x2 = gl_add(x2, s2[r]);
+        iz = gl_mul(iz, P.z);
+        izg = gl_mul(izg, P.zg);
+    }
+}
+void launch_deep(const u64* coef, const u64* hcoef, const DeepParams* dp, u64* bsum, u64* carry, u64* deep, int logn,
+                 int npoly, hipStream_t s) {
+    u64 n = 1ULL << logn;
+    u64 nthreads = (n + DEEP_PER_THREAD - 1) / DEEP_PER_THREAD;
+    int threads = nthreads < 256 ? (int)nthreads : 256;
+    int nblk = (int)((nthreads + threads - 1) / threads);
+    hipLaunchKernelGGL(deep_blocksum_kernel, dim3(nblk, npoly), dim3(threads), 0, s, coef, hcoef, dp, bsum, logn);
+    hipLaunchKernelGGL(deep_carry_kernel, dim3(npoly), dim3(64), 0, s, bsum, carry, nblk);
+    hipLaunchKernelGGL(deep_final_kernel, dim3(nblk, npoly), dim3(threads), 0, s, coef, hcoef, dp, carry, deep, logn);
+    XFG_CHECK_LAUNCH();
+}
+
+// ============================================================================ FRI fold
+// apply_drp for folding factor 8 with Winterfell's constant domain offset 7 on every layer:
+// row i = {v_k at 7 w_D^i zeta^k}; c = iDFT_8(v)/8 ; result = sum_j c_j (alpha / (7 w_D^i))^j
+struct FoldArgs {
+    const u64* vals;
+    u64 val_stride;
+    int coset_major, logn, logbeta;
+    u64 rows;
+    int logD;
+    const u64* alpha7;
+    u64* out;
+    u64 out_stride;
+    u64 winv8[4];  // w_8^-k, k < 4
+    u64 inv8;
+    Tables T;
+};
+__global__ __launch_bounds__(256) void fri_fold_kernel(FoldArgs a) {
+    const int proof = blockIdx.y;
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.rows) return;
+    const u64* base = a.vals + (u64)proof * a.val_stride;
+    u64 v[8];
+    // bit-reversed load for an in-register radix-2 DIT inverse DFT of size 8
+    const int br[8] = {0, 4, 2, 6, 1, 5, 3, 7};
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[k] = layer_at(base, a.coset_major, a.logn, a.logbeta, i + (u64)br[k] * a.rows);
+#pragma unroll
+    for (int s = 0; s < 3; s++) {
+        const int h = 1 << s;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            int pos = b & (h - 1), i0 = ((b >> s) << (s + 1)) + pos;
+            u64 w = a.winv8[pos << (2 - s)];
+            u64 u = v[i0], t = gl_mul(v[i0 + h], w);
+            v[i0] = gl_add(u, t);
+            v[i0 + h] = gl_sub(u, t);
+        }
+    }
+    // y = alpha * 7^-1 * w_D^-i ; Horner
+    u64 y = gl_mul(a.alpha7[proof], tw_ipow(a.T, a.logD, i));
+    u64 r = v[7];
+#pragma unroll
+    for (int j = 6; j >= 0; j--) r = gl_add(gl_mul(r, y), v[j]);
+    a.out[(u64)proof * a.out_stride + i] = gl_mul(r, a.inv8);
+}
+void launch_fri_fold(const u64* vals, u64 val_stride, bool coset_major, int logn, int logbeta, u64 rows, int logD,
+                     const u64* alpha7, u64* out, u64 out_stride, const Tables& T, int npoly, hipStream_t s) {
+    FoldArgs a;
+    a.vals = vals; a.val_stride = val_stride; a.coset_major = coset_major ? 1 : 0; a.logn = logn;
+    a.logbeta = logbeta; a.rows = rows; a.logD = logD; a.alpha7 = alpha7; a.out = out; a.out_stride = out_stride;
+    a.T = T;
+    u64 w8inv = gl_inv(gl_root(3));
+    for (int k = 0; k < 4; k++) a.winv8[k] = gl_pow(w8inv, k);
+    a.inv8 = gl_inv(8);
+    int threads = rows < 256 ? (int)rows : 256;
+    dim3 g((unsigned)((rows + threads - 1) / threads), npoly);
+    hipLaunchKernelGGL(fri_fold_kernel, g, dim3(threads), 0, s, a);
+    XFG_CHECK_LAUNCH();
+}
+
+// ============================================================================ gathers
+__global__ void gather_u64_kernel(const u64* src, const u64* idx, u64* dst, u64 count) {
+    u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) dst[i] = src[idx[i]];
+}
+__global__ void gather_digest_kernel(const Digest* src, const u64* idx, Digest* dst, u64 count) {
+    u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) dst[i] = src[idx[i]];
+}
+void launch_gather_u64(const u64* src, const u64* idx, u64* dst, u64 count, hipStream_t s) {
+    if (!count) return;
+    hipLaunchKernelGGL(gather_u64_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s, src, idx, dst, count);
+}
+void launch_gather_digest(const Digest* src, const u64* idx, Digest* dst, u64 count, hipStream_t s) {
+    if (!count) return;
+    hipLaunchKernelGGL(gather_digest_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s, src, idx, dst,
+                       count);
+}
+
+}  // namespace xfg

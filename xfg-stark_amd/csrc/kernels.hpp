@@ -1,0 +1,75 @@
+// Launch wrappers for the burn-proof STARK kernels (gfx950). Every wrapper enqueues on the given
+// stream and never synchronises; batch dimension = number of independent proofs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include "gl.hpp"
+#include "blake3.hpp"
+
+namespace xfg {
+
+// per-proof AIR constants (reference src/burn_mint_air.rs:54-71 order + Keccak constants)
+struct AirConst {
+    u64 pub[12];
+    u64 nullifier;
+    u64 commitment;
+    u64 pad[2];
+};
+
+// per-proof DEEP parameters: trace coefficients a_i, composition coefficient, OOD points and the
+// constant terms c1 = sum a_i T_i(z) + gamma H(z), c2 = sum a_i T_i(z g)
+struct DeepParams {
+    u64 a[7];
+    u64 gamma;
+    u64 z, zg, zinv, zginv;
+    u64 c1, c2;
+    u64 pad[4];
+};
+
+struct Tables {
+    const u64* tw;     // tw[e] = w_{2^LM}^e, e < 2^LM
+    int LM;
+    const u64* pow7;   // 7^j,  j < 2^LM
+    const u64* ipow7;  // 7^-j, j < 2^LM
+};
+
+// ---- NTT (four-step, natural order in/out) ----
+// forward LDE: coef[poly][n] -> out[poly][beta][n] (coset-major: out[p][t][m] = P(7 w_N^(t + beta m)))
+void launch_lde(const u64* coef, u64 coef_stride, u64* out, u64* scratch, int npoly, int logn, int logbeta,
+                const Tables& T, hipStream_t s);
+// inverse: evals[poly][n] at 7^off7 * w_n^i -> coefficients (first `keep` written, stride out_stride)
+void launch_interpolate(const u64* evals, u64 in_stride, u64* out, u64 out_stride, u64* scratch, int npoly, int logn,
+                        bool off7, u64 keep, const Tables& T, hipStream_t s);
+
+// ---- Merkle (heap layout: nodes[1] = root, nodes[L + i] = leaf i) ----
+// leaves = rows of an NC-column coset-major LDE (NC in {1, 7}); builds the in-block subtree levels
+void launch_leaves_lde(const u64* lde, int nc, Digest* nodes, u64 node_stride, int npoly, int logn, int logbeta,
+                       hipStream_t s);
+// FRI layer leaves: row i = values at natural indices i + k*rows, k < 8 (coset-major source when
+// coset_major, else natural); also writes in-block subtree levels
+void launch_fri_leaves(const u64* vals, u64 val_stride, bool coset_major, int logn, int logbeta, u64 rows,
+                       Digest* nodes, u64 node_stride, int npoly, hipStream_t s);
+// completes the tree above level `count` (nodes [count, 2count) present) up to the root
+void launch_tree_top(Digest* nodes, u64 node_stride, u64 count, int npoly, hipStream_t s);
+
+// ---- AIR ----
+void launch_trace_gen(const AirConst* air, u64* trace, int logn, int npoly, hipStream_t s);
+// composition evaluations over the CE domain 7*<w_2n> (natural order) from the trace LDE
+void launch_constraint_eval(const u64* lde, const AirConst* air, const u64* coeffs /*[B][15]*/, u64* ce, int logn,
+                            int logbeta, const Tables& T, int npoly, hipStream_t s);
+
+// ---- OOD / DEEP ----
+void launch_ood(const u64* coef, const u64* hcoef, const u64* zpts /*[B][2]*/, u64* partial, u64* ood /*[B][15]*/,
+                int logn, int npoly, hipStream_t s);
+void launch_deep(const u64* coef, const u64* hcoef, const DeepParams* dp, u64* bsum, u64* carry, u64* deep, int logn,
+                 int npoly, hipStream_t s);
+
+// ---- FRI ----
+void launch_fri_fold(const u64* vals, u64 val_stride, bool coset_major, int logn, int logbeta, u64 rows, int logD,
+                     const u64* alpha7 /*[B] = alpha * 7^-1*/, u64* out, u64 out_stride, const Tables& T, int npoly,
+                     hipStream_t s);
+
+// ---- openings ----
+void launch_gather_u64(const u64* src, const u64* idx, u64* dst, u64 count, hipStream_t s);
+void launch_gather_digest(const Digest* src, const u64* idx, Digest* dst, u64 count, hipStream_t s);
+
+}  // namespace xfg

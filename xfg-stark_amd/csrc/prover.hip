@@ -1,0 +1,1031 @@
+// Host orchestration of the MI355X burn-proof STARK prover + the C ABI (include/xfg_stark.h).
+//
+// Pipeline = Winterfell 0.8.3 `Prover::prove` as bound by the reference
+// (src/burn_mint_air.rs:479-531, src/burn_mint_prover.rs:62-129), batched over independent
+// proofs: every kernel launch covers all proofs of the batch, and the host only touches the
+// serial Fiat-Shamir steps (a few BLAKE3 calls per proof per round) between launch sets.
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/xfg_stark.h"
+#include "host_crypto.hpp"
+#include "kernels.hpp"
+
+namespace xfg {
+
+struct HipError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+#define HIPCHK(x)                                                                                  \
+    do {                                                                                           \
+        hipError_t e_ = (x);                                                                       \
+        if (e_ != hipSuccess)                                                                      \
+            throw HipError(std::string("HIP error ") + hipGetErrorString(e_) + " at " #x);        \
+    } while (0)
+
+static unsigned ilog2(u64 x) {
+    unsigned r = 0;
+    while ((1ULL << r) < x) r++;
+    return r;
+}
+static bool is_pow2(u64 x) { return x && !(x & (x - 1)); }
+
+// ------------------------------------------------------------------ options / context elements
+struct Opts {
+    u64 q, beta, grind, ext, fold, remdeg;
+};
+static Opts to_opts(const xfg_options* o) {
+    return Opts{o->num_queries, o->blowup_factor, o->grinding_factor, o->field_extension, o->fri_folding_factor,
+                o->fri_remainder_max_degree};
+}
+// ProofOptions::new validation (winter-air 0.8) + what this GPU path implements
+static const char* check_options(u64 n, const Opts& o) {
+    if (!is_pow2(n) || n < 8) return "trace length must be a power of two and at least 8";
+    if (n > (1ULL << 22)) return "trace length above 2^22 is not supported";
+    if (!is_pow2(o.beta) || o.beta < 2 || o.beta > 16) return "blowup factor must be a power of two in [2, 16]";
+    if (o.q < 1 || o.q > 255) return "number of queries must be in [1, 255]";
+    if (o.grind > 32) return "grinding factor cannot be greater than 32";
+    if (o.ext != 1) return "only FieldExtension::None is supported by this prover";
+    if (o.fold != 8) return "only FRI folding factor 8 is supported by this prover";
+    if (o.remdeg > 255 || !is_pow2(o.remdeg + 1)) return "FRI remainder max degree must be one less than a power of two";
+    if (o.q >= n * o.beta) return "number of queries must be smaller than the LDE domain size";
+    return nullptr;
+}
+static unsigned num_fri_layers(u64 N, const Opts& o) {
+    u64 maxrem = (o.remdeg + 1) * o.beta;
+    unsigned k = 0;
+    while (N > maxrem) {
+        N /= o.fold;
+        k++;
+    }
+    return k;
+}
+// Context::to_elements (TraceInfo, modulus bytes, options) -- DESIGN.md "Transcript"
+static void context_elements(u64 n, const Opts& o, u64* e) {
+    e[0] = 7ULL << 8;
+    e[1] = n;
+    e[2] = 1;
+    e[3] = 0xFFFFFFFFULL;
+    e[4] = (o.ext << 16) | (o.fold << 8) | o.remdeg;
+    e[5] = o.grind;
+    e[6] = o.beta;
+    e[7] = o.q;
+}
+
+// ------------------------------------------------------------------ DefaultRandomCoin<Blake3_256>
+struct Coin {
+    Digest seed;
+    u64 counter = 0;
+    void init(const u64* e, size_t cnt) {
+        seed = hash_elements(e, cnt);
+        counter = 0;
+    }
+    void reseed(const Digest& d) {
+        seed = b3_merge(seed, d);
+        counter = 0;
+    }
+    void reseed_int(u64 v) {
+        seed = merge_with_int(seed, v);
+        counter = 0;
+    }
+    Digest next() { return merge_with_int(seed, ++counter); }
+    bool draw(u64& out) {
+        for (int i = 0; i < 1000; i++) {
+            Digest v = next();
+            u64 x = (u64)v.w[0] | ((u64)v.w[1] << 32);
+            if (x < P) {
+                out = x;
+                return true;
+            }
+        }
+        return false;
+    }
+};
+static unsigned tz64(u64 x) { return x ? (unsigned)__builtin_ctzll(x) : 64; }
+
+// ------------------------------------------------------------------ marshalling
+static const u64 STANDARD_BURN = 8000000ULL, LARGE_BURN = 8000000000ULL;
+static u64 le_u32(const uint8_t* b) {
+    return (u64)b[0] | ((u64)b[1] << 8) | ((u64)b[2] << 16) | ((u64)b[3] << 24);
+}
+static u64 le_u64(const uint8_t* b) { return le_u32(b) | (le_u32(b + 4) << 32); }
+static void put_le64(uint8_t* d, u64 v) {
+    for (int i = 0; i < 8; i++) d[i] = (uint8_t)(v >> (8 * i));
+}
+
+// compute_nullifier / compute_recipient_hash / compute_commitment (src/burn_mint_air.rs:124-202)
+static void air_constants(const u64 pub[12], u64 secret, u64& nullifier, u64& commitment) {
+    uint8_t buf[160], h[32], rf[32];
+    size_t k = 0;
+    put_le64(buf, secret);
+    k = 8;
+    memcpy(buf + k, "nullifier", 9);
+    k += 9;
+    put_le64(buf + k, pub[0]);
+    k += 8;
+    keccak256(buf, k, h);
+    nullifier = le_u32(h);
+    k = 0;
+    put_le64(buf, pub[3]);
+    k = 8;
+    memcpy(buf + k, "ethereum-recipient", 18);
+    k += 18;
+    memcpy(buf + k, "fuego-to-heat-bridge", 20);
+    k += 20;
+    keccak256(buf, k, rf);
+    k = 0;
+    const u64 fields[3] = {secret, pub[0], pub[1]};
+    for (u64 f : fields) { put_le64(buf + k, f); k += 8; }
+    for (int i = 0; i < 4; i++) { put_le64(buf + k, pub[5 + i]); k += 8; }
+    memcpy(buf + k, rf, 32);
+    k += 32;
+    for (int i = 0; i < 3; i++) { put_le64(buf + k, pub[9 + i]); k += 8; }
+    memcpy(buf + k, "heat-commitment-v1", 18);
+    k += 18;
+    keccak256(buf, k, h);
+    commitment = le_u32(h);
+}
+
+// validate_inputs + prove_burn_mint marshalling (src/burn_mint_prover.rs:62-118, 132-221)
+static int marshal(const xfg_burn_inputs* in, AirConst& a, std::string& err) {
+    u64 legacy = le_u64(in->tx_prefix_hash);
+    if (in->burn_amount != STANDARD_BURN && in->burn_amount != LARGE_BURN) {
+        err = "Burn amount must be exactly 0.8 XFG (8,000,000 atomic units) or 800 XFG (8,000,000,000 atomic units)";
+        return XFG_INVALID_BURN_AMOUNT;
+    }
+    if (in->mint_amount != in->burn_amount) {
+        err = "Mint amount " + std::to_string(in->mint_amount) + " does not match burn amount " +
+              std::to_string(in->burn_amount) + " for 1:1 atomic unit conversion";
+        return XFG_MINT_MISMATCH;
+    }
+    if (legacy == 0) {
+        err = "Transaction hash must be greater than 0";
+        return XFG_ZERO_TX_HASH;
+    }
+    if (!in->recipient_address || in->recipient_len != 20) {
+        err = "Recipient address must be exactly 20 bytes";
+        return XFG_BAD_RECIPIENT_LEN;
+    }
+    if (!in->secret || in->secret_len < 4) {
+        err = "Secret must be at least 4 bytes";
+        return XFG_SHORT_SECRET;
+    }
+    if (in->secret_len < 8) {  // the reference slices secret[..8] and panics (:203-204)
+        err = "Secret must be at least 8 bytes (secret[..8] slice in secret_to_field_element)";
+        return XFG_SHORT_SECRET;
+    }
+    u64 secret = le_u32(in->secret);
+    uint8_t buf[29], h[32];
+    memcpy(buf, in->recipient_address, 20);
+    memcpy(buf + 20, "recipient", 9);
+    keccak256(buf, 29, h);
+    memset(&a, 0, sizeof a);
+    a.pub[0] = (uint32_t)in->burn_amount;
+    a.pub[1] = (uint32_t)in->mint_amount;
+    a.pub[2] = (uint32_t)legacy;
+    a.pub[3] = le_u32(h);
+    a.pub[4] = 0;
+    for (int i = 0; i < 4; i++) a.pub[5 + i] = le_u32(in->tx_prefix_hash + 4 * i);
+    a.pub[9] = in->network_id;
+    a.pub[10] = in->target_chain_id;
+    a.pub[11] = in->commitment_version;
+    air_constants(a.pub, secret, a.nullifier, a.commitment);
+    return XFG_OK;
+}
+
+// ------------------------------------------------------------------ byte writer
+struct BW {
+    std::vector<uint8_t> b;
+    void put(const void* p, size_t k) {
+        const uint8_t* q = (const uint8_t*)p;
+        b.insert(b.end(), q, q + k);
+    }
+    void u8(u64 v) { b.push_back((uint8_t)v); }
+    void u16(u64 v) { u8(v & 0xFF); u8((v >> 8) & 0xFF); }
+    void u32(u64 v) { for (int i = 0; i < 4; i++) u8((v >> (8 * i)) & 0xFF); }
+    void u64_(u64 v) { for (int i = 0; i < 8; i++) u8((v >> (8 * i)) & 0xFF); }
+    void digest(const Digest& d) {
+        uint8_t x[32];
+        digest_bytes(d, x);
+        put(x, 32);
+    }
+};
+
+// ------------------------------------------------------------------ batch Merkle openings
+// MerkleTree::prove_batch (winter-crypto 0.8.3) restated as heap-index lists: node vector i holds
+// the missing sibling leaf of normalised pair i, then the siblings met by the i-th entry of each
+// upper level's index list. Digests are gathered from HBM afterwards in this order.
+struct BatchOpening {
+    std::vector<std::vector<u64>> vecs;  // heap indices (leaf i -> L + i)
+};
+static BatchOpening plan_batch_opening(const std::vector<u64>& idx, u64 L) {
+    unsigned depth = ilog2(L);
+    std::vector<u64> norm;
+    for (u64 i : idx) norm.push_back(i & ~1ULL);
+    std::sort(norm.begin(), norm.end());
+    norm.erase(std::unique(norm.begin(), norm.end()), norm.end());
+    BatchOpening op;
+    op.vecs.resize(norm.size());
+    std::vector<u64> cur(norm.size());
+    for (size_t i = 0; i < norm.size(); i++) {
+        for (u64 leaf = norm[i]; leaf < norm[i] + 2; leaf++)
+            if (std::find(idx.begin(), idx.end(), leaf) == idx.end()) op.vecs[i].push_back(L + leaf);
+        cur[i] = (norm[i] + L) >> 1;
+    }
+    for (unsigned lvl = 1; lvl < depth; lvl++) {
+        std::vector<u64> nxt;
+        for (size_t i = 0; i < cur.size(); i++) {
+            u64 sib = cur[i] ^ 1;
+            if (i + 1 < cur.size() && cur[i + 1] == sib) i++;
+            else op.vecs[i].push_back(sib);
+            nxt.push_back(sib >> 1);
+        }
+        cur.swap(nxt);
+    }
+    return op;
+}
+static std::vector<u64> fold_positions(const std::vector<u64>& in, u64 target) {
+    std::vector<u64> out;
+    for (u64 p : in) {
+        u64 q = p % target;
+        if (std::find(out.begin(), out.end(), q) == out.end()) out.push_back(q);
+    }
+    return out;
+}
+
+// ------------------------------------------------------------------ device buffers
+template <class T>
+struct DBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    void ensure(size_t cnt) {
+        if (cnt <= n) return;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        HIPCHK(hipMalloc((void**)&p, std::max<size_t>(cnt, 1) * sizeof(T)));
+        n = cnt;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+struct TablesHost {
+    int LM = -1;
+    DBuf<u64> tw, pow7, ipow7;
+};
+
+static const char* STAGE_NAMES[] = {"trace_lde",     "trace_commit", "constraint_eval", "composition",
+                                    "comp_commit",   "ood",          "deep",            "fri",
+                                    "queries_gather", "host_total"};
+enum { ST_LDE, ST_TCOMMIT, ST_CE, ST_COMP, ST_CCOMMIT, ST_OOD, ST_DEEP, ST_FRI, ST_GATHER, ST_HOST, ST_COUNT };
+
+}  // namespace xfg
+
+struct xfg_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    bool timing = false;
+    double stage_ms[xfg::ST_COUNT] = {0};
+    hipEvent_t ev[xfg::ST_COUNT + 1] = {};
+    xfg::TablesHost tables;
+    // pooled device buffers
+    xfg::DBuf<xfg::AirConst> air;
+    xfg::DBuf<xfg::u64> coeffs, trace, coef, scratch, lde, ce, hcoef, hlde, zpts, partial, ood, bsum, carry, deep, f0,
+        alpha7, rem, gidx, gval, dn2;
+    xfg::DBuf<xfg::Digest> tnodes, hnodes, gdig, roots;
+    xfg::DBuf<xfg::DeepParams> dp;
+    std::vector<xfg::DBuf<xfg::u64>> flayer;
+    std::vector<xfg::DBuf<xfg::Digest>> fnodes;
+};
+
+namespace xfg {
+
+static void ensure_tables(xfg_ctx* c, int LM) {
+    if (c->tables.LM >= LM) return;
+    u64 M = 1ULL << LM;
+    std::vector<u64> tw(M), p7(M), ip7(M);
+    u64 w = gl_root(LM), x = 1, y = 1, z = 1, i7 = gl_inv(GEN);
+    for (u64 e = 0; e < M; e++) {
+        tw[e] = x;
+        p7[e] = y;
+        ip7[e] = z;
+        x = gl_mul(x, w);
+        y = gl_mul(y, GEN);
+        z = gl_mul(z, i7);
+    }
+    c->tables.tw.release();
+    c->tables.pow7.release();
+    c->tables.ipow7.release();
+    c->tables.tw.ensure(M);
+    c->tables.pow7.ensure(M);
+    c->tables.ipow7.ensure(M);
+    HIPCHK(hipMemcpy(c->tables.tw.p, tw.data(), M * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->tables.pow7.p, p7.data(), M * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->tables.ipow7.p, ip7.data(), M * 8, hipMemcpyHostToDevice));
+    c->tables.LM = LM;
+}
+static Tables tables_of(xfg_ctx* c) {
+    Tables T;
+    T.tw = c->tables.tw.p;
+    T.LM = c->tables.LM;
+    T.pow7 = c->tables.pow7.p;
+    T.ipow7 = c->tables.ipow7.p;
+    return T;
+}
+
+// D2H of the root (heap index 1) of B trees laid out with a per-proof stride
+static void fetch_roots(xfg_ctx* c, const Digest* nodes, u64 stride, int B, std::vector<Digest>& out) {
+    out.resize(B);
+    HIPCHK(hipMemcpy2DAsync(out.data(), sizeof(Digest), nodes + 1, stride * sizeof(Digest), sizeof(Digest), B,
+                            hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+}
+
+struct ProofJob {
+    AirConst air;
+    Coin coin;
+    std::vector<uint8_t> commitments;
+    u64 ood[15];
+    u64 nonce = 0;
+    std::vector<u64> pos;
+    std::vector<uint8_t> bytes;
+    int status = XFG_OK;
+};
+
+static void stage_mark(xfg_ctx* c, int k) {
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[k], c->stream));
+}
+
+// the batched prover: jobs[i].air filled; trace_host optional ([B][7][n], else generated on device)
+static void prove_jobs(xfg_ctx* c, std::vector<ProofJob>& jobs, const u64* trace_host, u64 n, const Opts& o) {
+    auto t_host0 = std::chrono::steady_clock::now();
+    const int B = (int)jobs.size();
+    const int logn = (int)ilog2(n), logbeta = (int)ilog2(o.beta);
+    const u64 beta = o.beta, N = n * beta;
+    const int logN = logn + logbeta;
+    const unsigned nl = num_fri_layers(N, o);
+    hipStream_t s = c->stream;
+    ensure_tables(c, logN);
+    const Tables T = tables_of(c);
+
+    // ---- buffers
+    c->air.ensure(B);
+    c->coeffs.ensure((size_t)B * 15);
+    c->trace.ensure((size_t)B * 7 * n);
+    c->coef.ensure((size_t)B * 7 * n);
+    c->scratch.ensure((size_t)B * 7 * N);
+    c->lde.ensure((size_t)B * 7 * N);
+    c->tnodes.ensure((size_t)B * 2 * N);
+    c->ce.ensure((size_t)B * 2 * n);
+    c->hcoef.ensure((size_t)B * n);
+    c->hlde.ensure((size_t)B * N);
+    c->hnodes.ensure((size_t)B * 2 * N);
+    c->zpts.ensure((size_t)B * 2);
+    c->partial.ensure((size_t)B * 15 * (n / 8 / 256 + 2));
+    c->ood.ensure((size_t)B * 15);
+    c->dp.ensure(B);
+    c->bsum.ensure((size_t)B * 2 * (n / 8 / 256 + 2));
+    c->carry.ensure((size_t)B * 2 * (n / 8 / 256 + 2));
+    c->deep.ensure((size_t)B * n);
+    c->f0.ensure((size_t)B * N);
+    c->alpha7.ensure(B);
+    c->dn2.ensure(B);
+    if (c->flayer.size() < nl + 1) {
+        c->flayer.resize(nl + 1);
+        c->fnodes.resize(nl + 1);
+    }
+    std::vector<u64> D(nl + 1);
+    D[0] = N;
+    for (unsigned l = 1; l <= nl; l++) D[l] = D[l - 1] / o.fold;
+    for (unsigned l = 0; l < nl; l++) {
+        c->fnodes[l].ensure((size_t)B * 2 * (D[l] / o.fold));
+        c->flayer[l + 1].ensure((size_t)B * D[l + 1]);
+    }
+    const u64 rem_len = N >> (3 * nl) >> logbeta;  // D_final / blowup
+    c->rem.ensure((size_t)B * std::max<u64>(rem_len, 1));
+
+    std::vector<AirConst> airs(B);
+    for (int b = 0; b < B; b++) airs[b] = jobs[b].air;
+    HIPCHK(hipMemcpyAsync(c->air.p, airs.data(), B * sizeof(AirConst), hipMemcpyHostToDevice, s));
+    // transcript seed: Context::to_elements || public inputs (ProverChannel::new)
+    for (auto& j : jobs) {
+        u64 e[20];
+        context_elements(n, o, e);
+        memcpy(e + 8, j.air.pub, 12 * 8);
+        j.coin.init(e, 20);
+        j.commitments.clear();
+    }
+
+    // ---- 1. trace LDE + commitment (DefaultTraceLde::new)
+    stage_mark(c, 0);
+    if (trace_host) HIPCHK(hipMemcpyAsync(c->trace.p, trace_host, (size_t)B * 7 * n * 8, hipMemcpyHostToDevice, s));
+    else launch_trace_gen(c->air.p, c->trace.p, logn, B, s);
+    launch_interpolate(c->trace.p, n, c->coef.p, n, c->scratch.p, B * 7, logn, false, n, T, s);
+    launch_lde(c->coef.p, n, c->lde.p, c->scratch.p, B * 7, logn, logbeta, T, s);
+    stage_mark(c, 1);
+    launch_leaves_lde(c->lde.p, 7, c->tnodes.p, 2 * N, B, logn, logbeta, s);
+    launch_tree_top(c->tnodes.p, 2 * N, n / std::min<u64>(n, 256), B, s);
+    std::vector<Digest> roots;
+    stage_mark(c, 2);
+    fetch_roots(c, c->tnodes.p, 2 * N, B, roots);
+
+    // ---- 2. constraint composition coefficients (7 transition + 8 boundary)
+    std::vector<u64> co((size_t)B * 15);
+    for (int b = 0; b < B; b++) {
+        auto& j = jobs[b];
+        uint8_t rb[32];
+        digest_bytes(roots[b], rb);
+        j.commitments.insert(j.commitments.end(), rb, rb + 32);
+        j.coin.reseed(roots[b]);
+        for (int k = 0; k < 15; k++)
+            if (!j.coin.draw(co[(size_t)b * 15 + k])) j.status = XFG_PROVER_ERROR;
+    }
+    HIPCHK(hipMemcpyAsync(c->coeffs.p, co.data(), co.size() * 8, hipMemcpyHostToDevice, s));
+
+    // ---- 3. constraint evaluation + composition polynomial + commitment
+    launch_constraint_eval(c->lde.p, c->air.p, c->coeffs.p, c->ce.p, logn, logbeta, T, B, s);
+    stage_mark(c, 3);
+    launch_interpolate(c->ce.p, 2 * n, c->hcoef.p, n, c->scratch.p, B, logn + 1, true, n, T, s);
+    launch_lde(c->hcoef.p, n, c->hlde.p, c->scratch.p, B, logn, logbeta, T, s);
+    stage_mark(c, 4);
+    launch_leaves_lde(c->hlde.p, 1, c->hnodes.p, 2 * N, B, logn, logbeta, s);
+    launch_tree_top(c->hnodes.p, 2 * N, n / std::min<u64>(n, 256), B, s);
+    stage_mark(c, 5);
+    fetch_roots(c, c->hnodes.p, 2 * N, B, roots);
+
+    // ---- 4. OOD point and frame
+    const u64 g = gl_root(logn);
+    std::vector<u64> zp((size_t)B * 2);
+    for (int b = 0; b < B; b++) {
+        auto& j = jobs[b];
+        uint8_t rb[32];
+        digest_bytes(roots[b], rb);
+        j.commitments.insert(j.commitments.end(), rb, rb + 32);
+        j.coin.reseed(roots[b]);
+        u64 z = 0;
+        if (!j.coin.draw(z)) j.status = XFG_PROVER_ERROR;
+        zp[2 * b] = z;
+        zp[2 * b + 1] = gl_mul(z, g);
+    }
+    HIPCHK(hipMemcpyAsync(c->zpts.p, zp.data(), zp.size() * 8, hipMemcpyHostToDevice, s));
+    launch_ood(c->coef.p, c->hcoef.p, c->zpts.p, c->partial.p, c->ood.p, logn, B, s);
+    std::vector<u64> ood((size_t)B * 15);
+    HIPCHK(hipMemcpyAsync(ood.data(), c->ood.p, ood.size() * 8, hipMemcpyDeviceToHost, s));
+    stage_mark(c, 6);
+    HIPCHK(hipStreamSynchronize(s));
+
+    // ---- 5. DEEP composition polynomial (coefficient form) + its LDE
+    std::vector<DeepParams> dps(B);
+    for (int b = 0; b < B; b++) {
+        auto& j = jobs[b];
+        memcpy(j.ood, &ood[(size_t)b * 15], 15 * 8);
+        j.coin.reseed(hash_elements(j.ood, 14));  // interleaved T_i(z), T_i(zg)
+        j.coin.reseed(hash_elements(j.ood + 14, 1));
+        DeepParams& P = dps[b];
+        memset(&P, 0, sizeof P);
+        for (int k = 0; k < 7; k++)
+            if (!j.coin.draw(P.a[k])) j.status = XFG_PROVER_ERROR;
+        if (!j.coin.draw(P.gamma)) j.status = XFG_PROVER_ERROR;
+        P.z = zp[2 * b];
+        P.zg = zp[2 * b + 1];
+        if (P.z == 0 || P.zg == 0) j.status = XFG_PROVER_ERROR;
+        P.zinv = P.z ? gl_inv(P.z) : 0;
+        P.zginv = P.zg ? gl_inv(P.zg) : 0;
+        u64 c1 = gl_mul(P.gamma, j.ood[14]), c2 = 0;
+        for (int k = 0; k < 7; k++) {
+            c1 = gl_add(c1, gl_mul(P.a[k], j.ood[2 * k]));
+            c2 = gl_add(c2, gl_mul(P.a[k], j.ood[2 * k + 1]));
+        }
+        P.c1 = c1;
+        P.c2 = c2;
+    }
+    HIPCHK(hipMemcpyAsync(c->dp.p, dps.data(), B * sizeof(DeepParams), hipMemcpyHostToDevice, s));
+    launch_deep(c->coef.p, c->hcoef.p, c->dp.p, c->bsum.p, c->carry.p, c->deep.p, logn, B, s);
+    launch_lde(c->deep.p, n, c->f0.p, c->scratch.p, B, logn, logbeta, T, s);
+    // degree check: deg(DEEP) == n - 2  <=>  coefficient n-2 != 0 (coefficient n-1 is 0 by construction)
+    HIPCHK(hipMemcpy2DAsync(c->dn2.p, 8, c->deep.p + (n - 2), n * 8, 8, B, hipMemcpyDeviceToDevice, s));
+    stage_mark(c, 7);
+
+    // ---- 6. FRI layers (FriProver::build_layers), folding factor 8
+    std::vector<u64> alpha7h(B);
+    const u64 inv7 = gl_inv(GEN);
+    for (unsigned l = 0; l < nl; l++) {
+        const u64 rows = D[l] / 8;
+        const bool cm = (l == 0);
+        const u64* src = cm ? c->f0.p : c->flayer[l].p;
+        const u64 sstride = cm ? N : D[l];
+        launch_fri_leaves(src, sstride, cm, logn, logbeta, rows, c->fnodes[l].p, 2 * rows, B, s);
+        launch_tree_top(c->fnodes[l].p, 2 * rows, rows / std::min<u64>(rows, 256), B, s);
+        fetch_roots(c, c->fnodes[l].p, 2 * rows, B, roots);
+        for (int b = 0; b < B; b++) {
+            auto& j = jobs[b];
+            uint8_t rb[32];
+            digest_bytes(roots[b], rb);
+            j.commitments.insert(j.commitments.end(), rb, rb + 32);
+            j.coin.reseed(roots[b]);
+            u64 a = 0;
+            if (!j.coin.draw(a)) j.status = XFG_PROVER_ERROR;
+            alpha7h[b] = gl_mul(a, inv7);
+        }
+        HIPCHK(hipMemcpyAsync(c->alpha7.p, alpha7h.data(), B * 8, hipMemcpyHostToDevice, s));
+        launch_fri_fold(src, sstride, cm, logn, logbeta, rows, (int)ilog2(D[l]), c->alpha7.p, c->flayer[l + 1].p,
+                        rows, T, B, s);
+    }
+    // remainder: interpolate the last layer over 7*<w_D>, keep D/blowup coefficients
+    // (with no folding layer this is the DEEP polynomial's own coefficients)
+    std::vector<u64> remh((size_t)B * rem_len);
+    if (nl > 0) {
+        launch_interpolate(c->flayer[nl].p, D[nl], c->rem.p, rem_len, c->scratch.p, B, (int)ilog2(D[nl]), true,
+                           rem_len, T, s);
+        HIPCHK(hipMemcpyAsync(remh.data(), c->rem.p, remh.size() * 8, hipMemcpyDeviceToHost, s));
+    } else {
+        HIPCHK(hipMemcpy2DAsync(remh.data(), rem_len * 8, c->deep.p, n * 8, rem_len * 8, B, hipMemcpyDeviceToHost, s));
+    }
+    std::vector<u64> dn2h(B);
+    HIPCHK(hipMemcpyAsync(dn2h.data(), c->dn2.p, B * 8, hipMemcpyDeviceToHost, s));
+    stage_mark(c, 8);
+    HIPCHK(hipStreamSynchronize(s));
+
+    // ---- 7. grinding + query positions, gather lists
+    std::vector<u64> vidx_lde, vidx_h, vidx_f0;
+    std::vector<std::vector<u64>> vidx_f(nl + 1);
+    std::vector<u64> didx_t, didx_h;
+    std::vector<std::vector<u64>> didx_f(nl + 1);
+    struct Layout {
+        std::vector<BatchOpening> ops;  // trace, comp, fri layers
+        std::vector<std::vector<u64>> fpos;
+    };
+    std::vector<Layout> lay(B);
+    for (int b = 0; b < B; b++) {
+        auto& j = jobs[b];
+        if (dn2h[b] == 0) j.status = XFG_PROVER_ERROR;  // assert_eq!(trace_length - 2, degree)
+        Digest rc = hash_elements(&remh[(size_t)b * rem_len], rem_len);
+        uint8_t rb[32];
+        digest_bytes(rc, rb);
+        j.commitments.insert(j.commitments.end(), rb, rb + 32);
+        j.coin.reseed(rc);
+        u64 nonce = 1;
+        while (tz64([&] { Digest h = merge_with_int(j.coin.seed, nonce); return (u64)h.w[0] | ((u64)h.w[1] << 32); }()) <
+               o.grind)
+            nonce++;
+        j.nonce = nonce;
+        j.coin.reseed_int(nonce);
+        std::vector<u64> pos(o.q);
+        for (u64 i = 0; i < o.q; i++) {
+            Digest h = j.coin.next();
+            pos[i] = ((u64)h.w[0] | ((u64)h.w[1] << 32)) & (N - 1);
+        }
+        std::sort(pos.begin(), pos.end());
+        pos.erase(std::unique(pos.begin(), pos.end()), pos.end());
+        j.pos = pos;
+        Layout& L = lay[b];
+        for (u64 k : pos) {
+            u64 t = k & (beta - 1), m = k >> logbeta;
+            for (int col = 0; col < 7; col++) vidx_lde.push_back((((u64)b * 7 + col) * beta + t) * n + m);
+            vidx_h.push_back(((u64)b * beta + t) * n + m);
+        }
+        L.ops.push_back(plan_batch_opening(pos, N));
+        L.ops.push_back(plan_batch_opening(pos, N));
+        for (auto& v : L.ops[0].vecs) for (u64 x : v) didx_t.push_back((u64)b * 2 * N + x);
+        for (auto& v : L.ops[1].vecs) for (u64 x : v) didx_h.push_back((u64)b * 2 * N + x);
+        std::vector<u64> fp = pos;
+        for (unsigned l = 0; l < nl; l++) {
+            u64 rows = D[l] / 8;
+            fp = fold_positions(fp, rows);
+            L.fpos.push_back(fp);
+            for (u64 i : fp)
+                for (u64 k = 0; k < 8; k++) {
+                    u64 K = i + k * rows;
+                    if (l == 0) vidx_f[0].push_back(((u64)b * beta + (K & (beta - 1))) * n + (K >> logbeta));
+                    else vidx_f[l].push_back((u64)b * D[l] + K);
+                }
+            L.ops.push_back(plan_batch_opening(fp, rows));
+            for (auto& v : L.ops.back().vecs) for (u64 x : v) didx_f[l].push_back((u64)b * 2 * rows + x);
+        }
+    }
+    // one index buffer, one value buffer, one digest buffer; segment per source
+    std::vector<u64> allidx;
+    std::vector<std::pair<size_t, size_t>> vseg, dseg;  // (offset, count)
+    auto add_seg = [&](const std::vector<u64>& v, std::vector<std::pair<size_t, size_t>>& seg) {
+        seg.push_back({allidx.size(), v.size()});
+        allidx.insert(allidx.end(), v.begin(), v.end());
+    };
+    add_seg(vidx_lde, vseg);
+    add_seg(vidx_h, vseg);
+    for (unsigned l = 0; l < nl; l++) add_seg(vidx_f[l], vseg);
+    size_t nvals = allidx.size();
+    add_seg(didx_t, dseg);
+    add_seg(didx_h, dseg);
+    for (unsigned l = 0; l < nl; l++) add_seg(didx_f[l], dseg);
+    size_t ndig = allidx.size() - nvals;
+    c->gidx.ensure(allidx.size());
+    c->gval.ensure(nvals);
+    c->gdig.ensure(ndig);
+    HIPCHK(hipMemcpyAsync(c->gidx.p, allidx.data(), allidx.size() * 8, hipMemcpyHostToDevice, s));
+    {
+        size_t vo = 0;
+        const u64* vsrc[2] = {c->lde.p, c->hlde.p};
+        for (size_t k = 0; k < vseg.size(); k++) {
+            const u64* src = k < 2 ? vsrc[k] : (k == 2 ? c->f0.p : c->flayer[k - 2].p);
+            launch_gather_u64(src, c->gidx.p + vseg[k].first, c->gval.p + vo, vseg[k].second, s);
+            vo += vseg[k].second;
+        }
+        size_t dof = 0;
+        for (size_t k = 0; k < dseg.size(); k++) {
+            const Digest* src = k == 0 ? c->tnodes.p : (k == 1 ? c->hnodes.p : c->fnodes[k - 2].p);
+            launch_gather_digest(src, c->gidx.p + dseg[k].first, c->gdig.p + dof, dseg[k].second, s);
+            dof += dseg[k].second;
+        }
+    }
+    std::vector<u64> gv(nvals);
+    std::vector<Digest> gd(ndig);
+    if (nvals) HIPCHK(hipMemcpyAsync(gv.data(), c->gval.p, nvals * 8, hipMemcpyDeviceToHost, s));
+    if (ndig) HIPCHK(hipMemcpyAsync(gd.data(), c->gdig.p, ndig * sizeof(Digest), hipMemcpyDeviceToHost, s));
+    stage_mark(c, 9);
+    HIPCHK(hipStreamSynchronize(s));
+
+    // ---- 8. StarkProof::to_bytes (DESIGN.md "Proof format")
+    size_t cur_lde = 0, cur_h = vidx_lde.size(), cur_t = 0, cur_hd = didx_t.size();
+    std::vector<size_t> cur_fv(nl), cur_fd(nl);
+    {
+        size_t off = vidx_lde.size() + vidx_h.size();
+        for (unsigned l = 0; l < nl; l++) { cur_fv[l] = off; off += vidx_f[l].size(); }
+        off = didx_t.size() + didx_h.size();
+        for (unsigned l = 0; l < nl; l++) { cur_fd[l] = off; off += didx_f[l].size(); }
+    }
+    auto write_paths = [&](BW& w, const BatchOpening& op, size_t& cursor) {
+        BW p;
+        p.u8(op.vecs.size());
+        for (auto& v : op.vecs) {
+            p.u8(v.size());
+            for (size_t k = 0; k < v.size(); k++) p.digest(gd[cursor++]);
+        }
+        w.u32(p.b.size());
+        w.put(p.b.data(), p.b.size());
+    };
+    for (int b = 0; b < B; b++) {
+        auto& j = jobs[b];
+        const u64 nu = j.pos.size();
+        BW w;
+        // Context
+        w.u8(7); w.u8(0); w.u8(logn); w.u16(0);
+        w.u8(8); w.u64_(P);
+        w.u8(o.q); w.u8(o.beta); w.u8(o.grind); w.u8(o.ext); w.u8(o.fold); w.u8(o.remdeg);
+        w.u8(nu);
+        w.u16(j.commitments.size());
+        w.put(j.commitments.data(), j.commitments.size());
+        // trace queries
+        w.u8(1);
+        w.u32(nu * 7 * 8);
+        for (u64 i = 0; i < nu * 7; i++) w.u64_(gv[cur_lde++]);
+        write_paths(w, lay[b].ops[0], cur_t);
+        // constraint queries
+        w.u32(nu * 8);
+        for (u64 i = 0; i < nu; i++) w.u64_(gv[cur_h++]);
+        write_paths(w, lay[b].ops[1], cur_hd);
+        // OOD frame
+        w.u16(1 + 14 * 8);
+        w.u8(2);
+        for (int k = 0; k < 14; k++) w.u64_(j.ood[k]);
+        w.u16(8);
+        w.u64_(j.ood[14]);
+        // FRI proof
+        w.u8(nl);
+        for (unsigned l = 0; l < nl; l++) {
+            u64 nk = lay[b].fpos[l].size();
+            w.u32(nk * 8 * 8);
+            for (u64 i = 0; i < nk * 8; i++) w.u64_(gv[cur_fv[l]++]);
+            write_paths(w, lay[b].ops[2 + l], cur_fd[l]);
+        }
+        w.u16(rem_len * 8);
+        for (u64 i = 0; i < rem_len; i++) w.u64_(remh[(size_t)b * rem_len + i]);
+        w.u8(0);
+        w.u64_(j.nonce);
+        j.bytes.swap(w.b);
+    }
+    if (c->timing) {
+        for (int k = 0; k < 9; k++) {
+            float ms = 0;
+            HIPCHK(hipEventElapsedTime(&ms, c->ev[k], c->ev[k + 1]));
+            c->stage_ms[k] = ms;
+        }
+        c->stage_ms[ST_HOST] =
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_host0).count();
+    }
+}
+
+static int copy_out(xfg_ctx* c, const std::vector<uint8_t>& bytes, uint8_t* out, size_t* out_len) {
+    if (!out_len) {
+        c->err = "out_len is NULL";
+        return XFG_INVALID_ARGUMENT;
+    }
+    if (!out || *out_len < bytes.size()) {
+        *out_len = bytes.size();
+        if (!out) return XFG_OK;
+        c->err = "output buffer too small";
+        return XFG_BUFFER_TOO_SMALL;
+    }
+    memcpy(out, bytes.data(), bytes.size());
+    *out_len = bytes.size();
+    return XFG_OK;
+}
+
+static int guarded(xfg_ctx* c, const std::function<int()>& f) {
+    try {
+        return f();
+    } catch (const HipError& e) {
+        c->err = e.what();
+        return XFG_DEVICE_ERROR;
+    } catch (const std::exception& e) {
+        c->err = std::string("Prover error: ") + e.what();
+        return XFG_PROVER_ERROR;
+    }
+}
+}  // namespace xfg
+
+using namespace xfg;
+
+extern "C" {
+
+xfg_ctx* xfg_ctx_create(int device_id) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device_id < 0 || device_id >= ndev) return nullptr;
+    if (hipSetDevice(device_id) != hipSuccess) return nullptr;
+    xfg_ctx* c = new xfg_ctx();
+    c->device = device_id;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return nullptr;
+    }
+    for (auto& e : c->ev) (void)hipEventCreate(&e);
+    return c;
+}
+
+void xfg_ctx_destroy(xfg_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    c->air.release();
+    for (auto* b : {&c->coeffs, &c->trace, &c->coef, &c->scratch, &c->lde, &c->ce, &c->hcoef, &c->hlde, &c->zpts,
+                    &c->partial, &c->ood, &c->bsum, &c->carry, &c->deep, &c->f0, &c->alpha7, &c->rem, &c->gidx,
+                    &c->gval, &c->dn2})
+        b->release();
+    for (auto* b : {&c->tnodes, &c->hnodes, &c->gdig, &c->roots}) b->release();
+    c->dp.release();
+    for (auto& b : c->flayer) b.release();
+    for (auto& b : c->fnodes) b.release();
+    c->tables.tw.release();
+    c->tables.pow7.release();
+    c->tables.ipow7.release();
+    for (auto& e : c->ev) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int xfg_default_options(xfg_options* o) {
+    if (!o) return XFG_INVALID_ARGUMENT;
+    // ProofOptions::new(42, 8, 4, FieldExtension::None, 8, 31) -- src/burn_mint_prover.rs:28-35
+    *o = xfg_options{42, 8, 4, 1, 8, 31};
+    return XFG_OK;
+}
+
+int xfg_last_error(const xfg_ctx* c, char* buf, size_t len) {
+    if (!c) return XFG_INVALID_ARGUMENT;
+    if (buf && len) {
+        size_t k = std::min(len - 1, c->err.size());
+        memcpy(buf, c->err.data(), k);
+        buf[k] = 0;
+    }
+    return (int)c->err.size();
+}
+
+size_t xfg_proof_size_bound(uint64_t n, const xfg_options* opts) {
+    if (!opts || !is_pow2(n)) return 0;
+    Opts o = to_opts(opts);
+    u64 N = n * o.beta, depth = ilog2(N);
+    unsigned L = num_fri_layers(N, o);
+    size_t s = 4096 + o.q * (7 * 8 + 8 + (size_t)L * o.fold * 8);
+    s += (size_t)(2 + L) * (1 + o.q * (1 + depth * 32));
+    s += (size_t)N * 8 / o.beta + 32 * (L + 3);
+    return s;
+}
+
+int xfg_burn_air_consts(const xfg_burn_inputs* in, xfg_air_consts* out) {
+    if (!in || !out) return XFG_INVALID_ARGUMENT;
+    AirConst a;
+    std::string err;
+    int st = marshal(in, a, err);
+    if (st) return st;
+    memcpy(out->pub_inputs, a.pub, sizeof a.pub);
+    out->nullifier = a.nullifier;
+    out->commitment = a.commitment;
+    return XFG_OK;
+}
+
+int xfg_prove_trace(xfg_ctx* c, const uint64_t* trace, uint32_t width, uint64_t n, const xfg_air_consts* air,
+                    const xfg_options* opts, uint8_t* out, size_t* out_len) {
+    if (!c) return XFG_INVALID_ARGUMENT;
+    c->err.clear();
+    if (!trace || !air || !opts || !out_len) {
+        c->err = "null argument";
+        return XFG_INVALID_ARGUMENT;
+    }
+    if (width != 7) {
+        c->err = "XfgBurnMintAir traces have 7 columns";
+        return XFG_INVALID_ARGUMENT;
+    }
+    Opts o = to_opts(opts);
+    if (const char* m = check_options(n, o)) {
+        c->err = std::string("Prover error: ") + m;
+        return XFG_PROVER_ERROR;
+    }
+    for (u64 i = 0; i < 7 * n; i++)
+        if (trace[i] >= P) {
+            c->err = "trace element is not a canonical field element";
+            return XFG_INVALID_ARGUMENT;
+        }
+    return guarded(c, [&]() -> int {
+        HIPCHK(hipSetDevice(c->device));
+        std::vector<ProofJob> jobs(1);
+        memset(&jobs[0].air, 0, sizeof(AirConst));
+        memcpy(jobs[0].air.pub, air->pub_inputs, sizeof air->pub_inputs);
+        jobs[0].air.nullifier = air->nullifier;
+        jobs[0].air.commitment = air->commitment;
+        prove_jobs(c, jobs, trace, n, o);
+        if (jobs[0].status) {
+            c->err = "Prover error: proof generation failed (degenerate transcript or DEEP degree)";
+            return jobs[0].status;
+        }
+        return copy_out(c, jobs[0].bytes, out, out_len);
+    });
+}
+
+int xfg_prove_batch(xfg_ctx* c, uint32_t count, const xfg_burn_inputs* inputs, uint64_t trace_length,
+                    const xfg_options* opts, uint8_t* const* outs, size_t* out_lens, int* statuses) {
+    if (!c) return XFG_INVALID_ARGUMENT;
+    c->err.clear();
+    if (!inputs || !opts || !out_lens || !statuses || count == 0) {
+        c->err = "null argument";
+        return XFG_INVALID_ARGUMENT;
+    }
+    u64 n = trace_length ? trace_length : 64;
+    Opts o = to_opts(opts);
+    if (const char* m = check_options(n, o)) {
+        c->err = std::string("Prover error: ") + m;
+        return XFG_PROVER_ERROR;
+    }
+    return guarded(c, [&]() -> int {
+        HIPCHK(hipSetDevice(c->device));
+        std::vector<ProofJob> jobs;
+        std::vector<uint32_t> which;
+        for (uint32_t i = 0; i < count; i++) {
+            AirConst a;
+            std::string err;
+            int st = marshal(&inputs[i], a, err);
+            statuses[i] = st;
+            if (st) {
+                c->err = err;
+                continue;
+            }
+            ProofJob j;
+            j.air = a;
+            jobs.push_back(std::move(j));
+            which.push_back(i);
+        }
+        if (!jobs.empty()) prove_jobs(c, jobs, nullptr, n, o);
+        for (size_t k = 0; k < jobs.size(); k++) {
+            uint32_t i = which[k];
+            if (jobs[k].status) {
+                statuses[i] = jobs[k].status;
+                continue;
+            }
+            size_t len = out_lens[i];
+            statuses[i] = copy_out(c, jobs[k].bytes, outs ? outs[i] : nullptr, &len);
+            out_lens[i] = len;
+        }
+        return XFG_OK;
+    });
+}
+
+int xfg_prove_burn_mint(xfg_ctx* c, const xfg_burn_inputs* in, uint64_t trace_length, const xfg_options* opts,
+                        uint8_t* out, size_t* out_len) {
+    if (!c) return XFG_INVALID_ARGUMENT;
+    if (!out_len) return XFG_INVALID_ARGUMENT;
+    int st = 0;
+    uint8_t* outs[1] = {out};
+    size_t lens[1] = {*out_len};
+    int r = xfg_prove_batch(c, 1, in, trace_length, opts, outs, lens, &st);
+    if (r) return r;
+    *out_len = lens[0];
+    return st;
+}
+
+int xfg_set_timing(xfg_ctx* c, int enabled) {
+    if (!c) return XFG_INVALID_ARGUMENT;
+    c->timing = enabled != 0;
+    return XFG_OK;
+}
+
+int xfg_stage_times(const xfg_ctx* c, double* ms, const char** names, int max) {
+    if (!c) return 0;
+    int k = std::min<int>(max, ST_COUNT);
+    for (int i = 0; i < k; i++) {
+        if (ms) ms[i] = c->stage_ms[i];
+        if (names) names[i] = STAGE_NAMES[i];
+    }
+    return k;
+}
+
+int xfg_bench_lde(xfg_ctx* c, uint32_t count, uint64_t n, uint32_t blowup, uint32_t iters, double* avg_ms) {
+    if (!c || !avg_ms || !is_pow2(n) || !is_pow2(blowup) || n < 8 || blowup < 2 || blowup > 16 || iters == 0)
+        return XFG_INVALID_ARGUMENT;
+    return guarded(c, [&]() -> int {
+        HIPCHK(hipSetDevice(c->device));
+        const int logn = (int)ilog2(n), logbeta = (int)ilog2(blowup);
+        const u64 N = n * blowup;
+        ensure_tables(c, logn + logbeta);
+        Tables T = tables_of(c);
+        c->coef.ensure((size_t)count * 7 * n);
+        c->scratch.ensure((size_t)count * 7 * N);
+        c->lde.ensure((size_t)count * 7 * N);
+        // deterministic canonical coefficients
+        std::vector<u64> h((size_t)count * 7 * n);
+        u64 x = 0x46472d535441524bULL;  // "FG-STARK"
+        for (auto& v : h) {
+            x += 0x9E3779B97F4A7C15ULL;
+            u64 z = x;
+            z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+            z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+            v = (z ^ (z >> 31)) % P;
+        }
+        HIPCHK(hipMemcpy(c->coef.p, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+        launch_lde(c->coef.p, n, c->lde.p, c->scratch.p, count * 7, logn, logbeta, T, c->stream);  // warm
+        HIPCHK(hipEventRecord(c->ev[0], c->stream));
+        for (uint32_t i = 0; i < iters; i++)
+            launch_lde(c->coef.p, n, c->lde.p, c->scratch.p, count * 7, logn, logbeta, T, c->stream);
+        HIPCHK(hipEventRecord(c->ev[1], c->stream));
+        HIPCHK(hipEventSynchronize(c->ev[1]));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+        *avg_ms = ms / iters;
+        return XFG_OK;
+    });
+}
+
+int xfg_debug_lde(xfg_ctx* c, const uint64_t* coef, uint32_t npoly, uint64_t n, uint32_t blowup, uint64_t* out) {
+    if (!c || !coef || !out || !is_pow2(n) || !is_pow2(blowup) || n < 8 || blowup < 2 || blowup > 16)
+        return XFG_INVALID_ARGUMENT;
+    return guarded(c, [&]() -> int {
+        HIPCHK(hipSetDevice(c->device));
+        const int logn = (int)ilog2(n), logbeta = (int)ilog2(blowup);
+        const u64 N = n * blowup;
+        ensure_tables(c, logn + logbeta);
+        Tables T = tables_of(c);
+        c->coef.ensure((size_t)npoly * n);
+        c->scratch.ensure((size_t)npoly * N);
+        c->lde.ensure((size_t)npoly * N);
+        HIPCHK(hipMemcpy(c->coef.p, coef, (size_t)npoly * n * 8, hipMemcpyHostToDevice));
+        launch_lde(c->coef.p, n, c->lde.p, c->scratch.p, npoly, logn, logbeta, T, c->stream);
+        std::vector<u64> cm((size_t)npoly * N);
+        HIPCHK(hipMemcpyAsync(cm.data(), c->lde.p, cm.size() * 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        for (u64 p = 0; p < npoly; p++)  // coset-major -> natural order
+            for (u64 t = 0; t < blowup; t++)
+                for (u64 m = 0; m < n; m++) out[p * N + t + blowup * m] = cm[(p * blowup + t) * n + m];
+        return XFG_OK;
+    });
+}
+
+int xfg_debug_interpolate(xfg_ctx* c, const uint64_t* evals, uint32_t npoly, uint64_t n, int offset7, uint64_t* out) {
+    if (!c || !evals || !out || !is_pow2(n) || n < 8) return XFG_INVALID_ARGUMENT;
+    return guarded(c, [&]() -> int {
+        HIPCHK(hipSetDevice(c->device));
+        const int logn = (int)ilog2(n);
+        ensure_tables(c, std::max(logn, c->tables.LM));
+        Tables T = tables_of(c);
+        c->trace.ensure((size_t)npoly * n);
+        c->coef.ensure((size_t)npoly * n);
+        c->scratch.ensure((size_t)npoly * n);
+        HIPCHK(hipMemcpy(c->trace.p, evals, (size_t)npoly * n * 8, hipMemcpyHostToDevice));
+        launch_interpolate(c->trace.p, n, c->coef.p, n, c->scratch.p, npoly, logn, offset7 != 0, n, T, c->stream);
+        HIPCHK(hipMemcpyAsync(out, c->coef.p, (size_t)npoly * n * 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        return XFG_OK;
+    });
+}
+
+}  // extern "C"

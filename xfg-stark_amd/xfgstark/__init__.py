@@ -1,0 +1,300 @@
+"""xfgstark -- Python mirror of the reference prover API over the MI355X C ABI (libxfgstark.so).
+
+Mirrors reference src/burn_mint_prover.rs (XfgBurnMintProver::new / with_options /
+prove_burn_mint / get_proof_size / security_parameter / proof_options) and the Winterfell
+ProofOptions / StarkProof surface it returns. All proving runs in libxfgstark.so (HIP kernels
+for gfx950); there is no CPU fallback: if the library is missing this module fails to import, and
+without a GPU the prover constructor raises.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_PKG = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(_PKG, "libxfgstark.so")
+HEADER_PATH = os.path.join(os.path.dirname(_PKG), "include", "xfg_stark.h")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"libxfgstark.so not built at {LIB_PATH}: run `make -C xfg-stark_amd` "
+                      "(or __graft_entry__.build()); the prover has no CPU fallback")
+
+_lib = C.CDLL(LIB_PATH)
+
+STATUS = {0: "OK", 1: "INVALID_BURN_AMOUNT", 2: "MINT_MISMATCH", 3: "ZERO_TX_HASH", 4: "BAD_RECIPIENT_LEN",
+          5: "SHORT_SECRET", 6: "PROVER_ERROR", 7: "DEVICE_ERROR", 8: "BUFFER_TOO_SMALL", 9: "INVALID_ARGUMENT"}
+
+
+class _Options(C.Structure):
+    _fields_ = [("num_queries", C.c_uint32), ("blowup_factor", C.c_uint32), ("grinding_factor", C.c_uint32),
+                ("field_extension", C.c_uint32), ("fri_folding_factor", C.c_uint32),
+                ("fri_remainder_max_degree", C.c_uint32)]
+
+
+class _BurnInputs(C.Structure):
+    _fields_ = [("burn_amount", C.c_uint64), ("mint_amount", C.c_uint64), ("tx_prefix_hash", C.c_uint8 * 32),
+                ("recipient_address", C.c_char_p), ("recipient_len", C.c_size_t), ("secret", C.c_char_p),
+                ("secret_len", C.c_size_t), ("network_id", C.c_uint32), ("target_chain_id", C.c_uint32),
+                ("commitment_version", C.c_uint32)]
+
+
+class _AirConsts(C.Structure):
+    _fields_ = [("pub_inputs", C.c_uint64 * 12), ("nullifier", C.c_uint64), ("commitment", C.c_uint64)]
+
+
+_u64p = C.POINTER(C.c_uint64)
+_u8p = C.POINTER(C.c_uint8)
+_lib.xfg_ctx_create.restype = C.c_void_p
+_lib.xfg_ctx_create.argtypes = [C.c_int]
+_lib.xfg_ctx_destroy.argtypes = [C.c_void_p]
+_lib.xfg_default_options.argtypes = [C.POINTER(_Options)]
+_lib.xfg_last_error.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t]
+_lib.xfg_proof_size_bound.restype = C.c_size_t
+_lib.xfg_proof_size_bound.argtypes = [C.c_uint64, C.POINTER(_Options)]
+_lib.xfg_prove_burn_mint.argtypes = [C.c_void_p, C.POINTER(_BurnInputs), C.c_uint64, C.POINTER(_Options), _u8p,
+                                     C.POINTER(C.c_size_t)]
+_lib.xfg_prove_trace.argtypes = [C.c_void_p, _u64p, C.c_uint32, C.c_uint64, C.POINTER(_AirConsts),
+                                 C.POINTER(_Options), _u8p, C.POINTER(C.c_size_t)]
+_lib.xfg_prove_batch.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(_BurnInputs), C.c_uint64, C.POINTER(_Options),
+                                 C.POINTER(_u8p), C.POINTER(C.c_size_t), C.POINTER(C.c_int)]
+_lib.xfg_burn_air_consts.argtypes = [C.POINTER(_BurnInputs), C.POINTER(_AirConsts)]
+_lib.xfg_set_timing.argtypes = [C.c_void_p, C.c_int]
+_lib.xfg_stage_times.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_char_p), C.c_int]
+_lib.xfg_bench_lde.argtypes = [C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.POINTER(C.c_double)]
+_lib.xfg_debug_lde.argtypes = [C.c_void_p, _u64p, C.c_uint32, C.c_uint64, C.c_uint32, _u64p]
+_lib.xfg_debug_interpolate.argtypes = [C.c_void_p, _u64p, C.c_uint32, C.c_uint64, C.c_int, _u64p]
+
+
+class XfgStarkError(Exception):
+    """XfgStarkError::CryptoError(String) (reference src/lib.rs:66-110); `.status` is the C-ABI code."""
+
+    def __init__(self, status, message):
+        super().__init__(message)
+        self.status = status
+        self.kind = STATUS.get(status, str(status))
+
+
+class FieldExtension:
+    NONE = 1
+    QUADRATIC = 2
+    CUBIC = 3
+
+
+class ProofOptions:
+    """winterfell::ProofOptions::new(num_queries, blowup_factor, grinding_factor, field_extension,
+    fri_folding_factor, fri_remainder_max_degree) -- argument order of winter-air 0.8."""
+
+    def __init__(self, num_queries, blowup_factor, grinding_factor, field_extension, fri_folding_factor,
+                 fri_remainder_max_degree):
+        self.num_queries = num_queries
+        self.blowup_factor = blowup_factor
+        self.grinding_factor = grinding_factor
+        self.field_extension = field_extension
+        self.fri_folding_factor = fri_folding_factor
+        self.fri_remainder_max_degree = fri_remainder_max_degree
+
+    @classmethod
+    def reference(cls):
+        """XfgBurnMintProver::new's ProofOptions::new(42, 8, 4, None, 8, 31) (src/burn_mint_prover.rs:28-35)."""
+        o = _Options()
+        _lib.xfg_default_options(C.byref(o))
+        return cls(o.num_queries, o.blowup_factor, o.grinding_factor, o.field_extension, o.fri_folding_factor,
+                   o.fri_remainder_max_degree)
+
+    def _c(self):
+        return _Options(self.num_queries, self.blowup_factor, self.grinding_factor, self.field_extension,
+                        self.fri_folding_factor, self.fri_remainder_max_degree)
+
+    def __repr__(self):
+        return ("ProofOptions(num_queries={0.num_queries}, blowup_factor={0.blowup_factor}, grinding_factor="
+                "{0.grinding_factor}, field_extension={0.field_extension}, fri_folding_factor="
+                "{0.fri_folding_factor}, fri_remainder_max_degree={0.fri_remainder_max_degree})").format(self)
+
+
+class StarkProof:
+    """Serialized winterfell::StarkProof (to_bytes layout: DESIGN.md "Proof format")."""
+
+    def __init__(self, data: bytes):
+        self._data = bytes(data)
+
+    def to_bytes(self) -> bytes:
+        return self._data
+
+    def __len__(self):
+        return len(self._data)
+
+    def __eq__(self, other):
+        return isinstance(other, StarkProof) and other._data == self._data
+
+
+def burn_inputs(burn_amount, mint_amount, tx_prefix_hash, recipient_address, secret, network_id=1,
+                target_chain_id=42161, commitment_version=1):
+    """pack prove_burn_mint arguments; keeps the referenced byte strings alive on the struct"""
+    tx = bytes(tx_prefix_hash)
+    if len(tx) != 32:
+        raise XfgStarkError(9, "tx_prefix_hash must be 32 bytes ([u8; 32])")
+    s = _BurnInputs()
+    s.burn_amount = burn_amount
+    s.mint_amount = mint_amount
+    s.tx_prefix_hash = (C.c_uint8 * 32)(*tx)
+    rcpt, sec = bytes(recipient_address), bytes(secret)
+    s._keep = (rcpt, sec)
+    s.recipient_address = rcpt
+    s.recipient_len = len(rcpt)
+    s.secret = sec
+    s.secret_len = len(sec)
+    s.network_id = network_id
+    s.target_chain_id = target_chain_id
+    s.commitment_version = commitment_version
+    return s
+
+
+def air_consts(burn_amount, mint_amount, tx_prefix_hash, recipient_address, secret, network_id=1,
+               target_chain_id=42161, commitment_version=1):
+    """(public inputs[12], nullifier, commitment) exactly as the prover derives them (host-side)."""
+    s = burn_inputs(burn_amount, mint_amount, tx_prefix_hash, recipient_address, secret, network_id,
+                    target_chain_id, commitment_version)
+    a = _AirConsts()
+    st = _lib.xfg_burn_air_consts(C.byref(s), C.byref(a))
+    if st:
+        raise XfgStarkError(st, STATUS[st])
+    return list(a.pub_inputs), a.nullifier, a.commitment
+
+
+def exported_symbols():
+    return [name for name in dir(_lib)]
+
+
+class XfgBurnMintProver:
+    """reference XfgBurnMintProver (src/burn_mint_prover.rs:18-244) on one MI355X device."""
+
+    def __init__(self, security_parameter=128, device=0, proof_options=None):
+        self._security_parameter = security_parameter
+        self._options = proof_options or ProofOptions.reference()
+        self._ctx = _lib.xfg_ctx_create(device)
+        if not self._ctx:
+            raise XfgStarkError(7, f"no HIP device {device} available for libxfgstark (no CPU fallback)")
+
+    @classmethod
+    def new(cls, security_parameter=128, device=0):
+        return cls(security_parameter, device)
+
+    @classmethod
+    def with_options(cls, security_parameter, proof_options, device=0):
+        return cls(security_parameter, device, proof_options)
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            _lib.xfg_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        self.close()
+
+    def _err(self, st):
+        buf = C.create_string_buffer(1024)
+        _lib.xfg_last_error(self._ctx, buf, 1024)
+        return XfgStarkError(st, buf.value.decode() or STATUS.get(st, str(st)))
+
+    def security_parameter(self):
+        return self._security_parameter
+
+    def proof_options(self):
+        return self._options
+
+    def get_proof_size(self, proof: StarkProof) -> int:
+        return len(proof.to_bytes())
+
+    def prove_burn_mint(self, burn_amount, mint_amount, tx_prefix_hash, recipient_address, secret, network_id=1,
+                        target_chain_id=42161, commitment_version=1, trace_length=64) -> StarkProof:
+        s = burn_inputs(burn_amount, mint_amount, tx_prefix_hash, recipient_address, secret, network_id,
+                        target_chain_id, commitment_version)
+        o = self._options._c()
+        cap = _lib.xfg_proof_size_bound(trace_length, C.byref(o))
+        buf = C.create_string_buffer(cap)
+        ln = C.c_size_t(cap)
+        st = _lib.xfg_prove_burn_mint(self._ctx, C.byref(s), trace_length, C.byref(o), C.cast(buf, _u8p), C.byref(ln))
+        if st:
+            raise self._err(st)
+        return StarkProof(C.string_at(buf, ln.value))
+
+    def prove_trace(self, trace, pub_inputs, nullifier, commitment) -> StarkProof:
+        """ExecutionTrace-level proving; trace = 7 columns of n canonical u64 (column-major)."""
+        import numpy as np
+        tr = np.ascontiguousarray(np.asarray(trace, dtype=np.uint64))
+        width, n = tr.shape
+        a = _AirConsts()
+        a.pub_inputs = (C.c_uint64 * 12)(*pub_inputs)
+        a.nullifier = nullifier
+        a.commitment = commitment
+        o = self._options._c()
+        cap = _lib.xfg_proof_size_bound(n, C.byref(o))
+        buf = C.create_string_buffer(cap)
+        ln = C.c_size_t(cap)
+        st = _lib.xfg_prove_trace(self._ctx, tr.ctypes.data_as(_u64p), width, n, C.byref(a), C.byref(o),
+                                  C.cast(buf, _u8p), C.byref(ln))
+        if st:
+            raise self._err(st)
+        return StarkProof(C.string_at(buf, ln.value))
+
+    def prove_batch(self, inputs, trace_length=64):
+        """list of dicts of prove_burn_mint kwargs -> list of StarkProof | XfgStarkError (per proof)."""
+        k = len(inputs)
+        arr = (_BurnInputs * k)()
+        keep = []
+        for i, kw in enumerate(inputs):
+            s = burn_inputs(**kw)
+            keep.append(s._keep)
+            arr[i] = s
+        o = self._options._c()
+        cap = _lib.xfg_proof_size_bound(trace_length, C.byref(o))
+        big = C.create_string_buffer(cap * k)
+        base = C.addressof(big)
+        outs = (_u8p * k)(*[C.cast(base + i * cap, _u8p) for i in range(k)])
+        lens = (C.c_size_t * k)(*([cap] * k))
+        sts = (C.c_int * k)()
+        st = _lib.xfg_prove_batch(self._ctx, k, arr, trace_length, C.byref(o), outs, lens, sts)
+        if st:
+            raise self._err(st)
+        res = []
+        for i in range(k):
+            if sts[i]:
+                res.append(XfgStarkError(sts[i], STATUS.get(sts[i])))
+            else:
+                res.append(StarkProof(C.string_at(base + i * cap, lens[i])))
+        return res
+
+    # ---- instrumentation
+    def set_timing(self, on=True):
+        _lib.xfg_set_timing(self._ctx, 1 if on else 0)
+
+    def stage_times(self):
+        ms = (C.c_double * 16)()
+        names = (C.c_char_p * 16)()
+        k = _lib.xfg_stage_times(self._ctx, ms, names, 16)
+        return {names[i].decode(): ms[i] for i in range(k)}
+
+    def bench_lde(self, count, n, blowup, iters):
+        avg = C.c_double()
+        st = _lib.xfg_bench_lde(self._ctx, count, n, blowup, iters, C.byref(avg))
+        if st:
+            raise self._err(st)
+        return avg.value
+
+    def debug_lde(self, coef, n, blowup):
+        import numpy as np
+        c = np.ascontiguousarray(np.asarray(coef, dtype=np.uint64)).reshape(-1, n)
+        out = np.zeros((c.shape[0], n * blowup), dtype=np.uint64)
+        st = _lib.xfg_debug_lde(self._ctx, c.ctypes.data_as(_u64p), c.shape[0], n, blowup, out.ctypes.data_as(_u64p))
+        if st:
+            raise self._err(st)
+        return out
+
+    def debug_interpolate(self, evals, n, offset7=False):
+        import numpy as np
+        e = np.ascontiguousarray(np.asarray(evals, dtype=np.uint64)).reshape(-1, n)
+        out = np.zeros_like(e)
+        st = _lib.xfg_debug_interpolate(self._ctx, e.ctypes.data_as(_u64p), e.shape[0], n, 1 if offset7 else 0,
+                                        out.ctypes.data_as(_u64p))
+        if st:
+            raise self._err(st)
+        return out
