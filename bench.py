@@ -139,8 +139,12 @@ def main():
     n = 1 << args.log_n
     per = args.per_gpu
 
+    call_s = []
+
     def prove_fn(kws):
+        t = time.perf_counter()
         res = prover.prove_batch(kws, trace_length=n)
+        call_s.append(time.perf_counter() - t)
         for r in res:
             if isinstance(r, Exception):
                 raise r
@@ -208,6 +212,7 @@ def main():
                          "kernel": "trace LDE (ntt_cols_kernel + ntt_rows_kernel), 7 columns x "
                                    f"{per} proofs, {lde_ms:.3f} ms/launch-set, {lde_bytes} algorithmic B"},
             "stage_ms_one_batch": prover_stage,
+            "prove_call_ms_mean": round(1e3 * sum(call_s[args.warmup:]) / max(1, len(call_s) - args.warmup), 3),
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)

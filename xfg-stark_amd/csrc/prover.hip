@@ -14,6 +14,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/xfg_stark.h"
@@ -206,18 +207,16 @@ static int marshal(const xfg_burn_inputs* in, AirConst& a, std::string& err) {
 struct BW {
     std::vector<uint8_t> b;
     void put(const void* p, size_t k) {
-        const uint8_t* q = (const uint8_t*)p;
-        b.insert(b.end(), q, q + k);
+        size_t o = b.size();
+        b.resize(o + k);
+        memcpy(b.data() + o, p, k);
     }
     void u8(u64 v) { b.push_back((uint8_t)v); }
-    void u16(u64 v) { u8(v & 0xFF); u8((v >> 8) & 0xFF); }
-    void u32(u64 v) { for (int i = 0; i < 4; i++) u8((v >> (8 * i)) & 0xFF); }
-    void u64_(u64 v) { for (int i = 0; i < 8; i++) u8((v >> (8 * i)) & 0xFF); }
-    void digest(const Digest& d) {
-        uint8_t x[32];
-        digest_bytes(d, x);
-        put(x, 32);
-    }
+    void u16(u64 v) { uint16_t x = (uint16_t)v; put(&x, 2); }  // little-endian host
+    void u32(u64 v) { uint32_t x = (uint32_t)v; put(&x, 4); }
+    void u64_(u64 v) { put(&v, 8); }
+    void u64s(const u64* v, size_t k) { put(v, 8 * k); }
+    void digest(const Digest& d) { put(d.w, 32); }  // LE words == digest bytes
 };
 
 // ------------------------------------------------------------------ batch Merkle openings
@@ -272,14 +271,39 @@ struct DBuf {
         if (p) (void)hipFree(p);
         p = nullptr;
         n = 0;
-        HIPCHK(hipMalloc((void**)&p, std::max<size_t>(cnt, 1) * sizeof(T)));
-        n = cnt;
+        size_t want = std::max<size_t>(cnt + cnt / 8, 1);
+        HIPCHK(hipMalloc((void**)&p, want * sizeof(T)));
+        n = want;
     }
     void release() {
         if (p) (void)hipFree(p);
         p = nullptr;
         n = 0;
     }
+};
+
+// pinned host staging (hipHostMalloc) so D2H/H2D copies are true async DMA, grown with headroom
+template <class T>
+struct HBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    T* ensure(size_t cnt) {
+        if (cnt <= n) return p;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+        size_t want = cnt + cnt / 4 + 16;
+        HIPCHK(hipHostMalloc((void**)&p, want * sizeof(T), hipHostMallocDefault));
+        n = want;
+        return p;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    T& operator[](size_t i) { return p[i]; }
+    T* data() { return p; }
 };
 
 struct TablesHost {
@@ -292,24 +316,49 @@ static const char* STAGE_NAMES[] = {"trace_lde",     "trace_commit", "constraint
                                     "queries_gather", "host_total"};
 enum { ST_LDE, ST_TCOMMIT, ST_CE, ST_COMP, ST_CCOMMIT, ST_OOD, ST_DEEP, ST_FRI, ST_GATHER, ST_HOST, ST_COUNT };
 
+// one lane = one HIP stream + its pooled device buffers + one host thread; a batch is split
+// across lanes so one lane's host-side Fiat-Shamir / serialisation overlaps another's kernels
+struct Lane {
+    hipStream_t stream = nullptr;
+    bool timing = false;
+    double stage_ms[ST_COUNT] = {0};
+    hipEvent_t ev[ST_COUNT + 1] = {};
+    DBuf<AirConst> air;
+    DBuf<u64> coeffs, trace, coef, scratch, lde, ce, hcoef, hlde, zpts, partial, ood, bsum, carry, deep, f0, alpha7,
+        rem, gidx, gval, dn2;
+    DBuf<Digest> tnodes, hnodes, gdig;
+    DBuf<DeepParams> dp;
+    std::vector<DBuf<u64>> flayer;
+    std::vector<DBuf<Digest>> fnodes;
+    // pinned host staging
+    HBuf<Digest> h_roots, h_gd;
+    HBuf<u64> h_co, h_zp, h_ood, h_a7, h_rem, h_dn2, h_idx, h_gv;
+    HBuf<AirConst> h_air;
+    HBuf<DeepParams> h_dp;
+    void release() {
+        for (auto* b : {&h_roots, &h_gd}) b->release();
+        for (auto* b : {&h_co, &h_zp, &h_ood, &h_a7, &h_rem, &h_dn2, &h_idx, &h_gv}) b->release();
+        h_air.release();
+        h_dp.release();
+        air.release();
+        for (auto* b : {&coeffs, &trace, &coef, &scratch, &lde, &ce, &hcoef, &hlde, &zpts, &partial, &ood, &bsum,
+                        &carry, &deep, &f0, &alpha7, &rem, &gidx, &gval, &dn2})
+            b->release();
+        for (auto* b : {&tnodes, &hnodes, &gdig}) b->release();
+        dp.release();
+        for (auto& b : flayer) b.release();
+        for (auto& b : fnodes) b.release();
+    }
+};
+
 }  // namespace xfg
 
 struct xfg_ctx {
     int device = 0;
-    hipStream_t stream = nullptr;
     std::string err;
     bool timing = false;
-    double stage_ms[xfg::ST_COUNT] = {0};
-    hipEvent_t ev[xfg::ST_COUNT + 1] = {};
     xfg::TablesHost tables;
-    // pooled device buffers
-    xfg::DBuf<xfg::AirConst> air;
-    xfg::DBuf<xfg::u64> coeffs, trace, coef, scratch, lde, ce, hcoef, hlde, zpts, partial, ood, bsum, carry, deep, f0,
-        alpha7, rem, gidx, gval, dn2;
-    xfg::DBuf<xfg::Digest> tnodes, hnodes, gdig, roots;
-    xfg::DBuf<xfg::DeepParams> dp;
-    std::vector<xfg::DBuf<xfg::u64>> flayer;
-    std::vector<xfg::DBuf<xfg::Digest>> fnodes;
+    std::vector<std::unique_ptr<xfg::Lane>> lanes;
 };
 
 namespace xfg {
@@ -348,9 +397,8 @@ static Tables tables_of(xfg_ctx* c) {
 }
 
 // D2H of the root (heap index 1) of B trees laid out with a per-proof stride
-static void fetch_roots(xfg_ctx* c, const Digest* nodes, u64 stride, int B, std::vector<Digest>& out) {
-    out.resize(B);
-    HIPCHK(hipMemcpy2DAsync(out.data(), sizeof(Digest), nodes + 1, stride * sizeof(Digest), sizeof(Digest), B,
+static void fetch_roots(Lane* c, const Digest* nodes, u64 stride, int B, Digest* out) {
+    HIPCHK(hipMemcpy2DAsync(out, sizeof(Digest), nodes + 1, stride * sizeof(Digest), sizeof(Digest), B,
                             hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
 }
@@ -366,21 +414,25 @@ struct ProofJob {
     int status = XFG_OK;
 };
 
-static void stage_mark(xfg_ctx* c, int k) {
+static void stage_mark(Lane* c, int k) {
     if (c->timing) HIPCHK(hipEventRecord(c->ev[k], c->stream));
 }
 
 // the batched prover: jobs[i].air filled; trace_host optional ([B][7][n], else generated on device)
-static void prove_jobs(xfg_ctx* c, std::vector<ProofJob>& jobs, const u64* trace_host, u64 n, const Opts& o) {
+static void prove_lane(Lane* c, const Tables& T, ProofJob* jobs_p, int B, const u64* trace_host, u64 n,
+                       const Opts& o) {
     auto t_host0 = std::chrono::steady_clock::now();
-    const int B = (int)jobs.size();
+    struct JobSpan {
+        ProofJob* p;
+        int k;
+        ProofJob& operator[](int i) { return p[i]; }
+        ProofJob* begin() { return p; }
+        ProofJob* end() { return p + k; }
+    } jobs{jobs_p, B};
     const int logn = (int)ilog2(n), logbeta = (int)ilog2(o.beta);
     const u64 beta = o.beta, N = n * beta;
-    const int logN = logn + logbeta;
     const unsigned nl = num_fri_layers(N, o);
     hipStream_t s = c->stream;
-    ensure_tables(c, logN);
-    const Tables T = tables_of(c);
 
     // ---- buffers
     c->air.ensure(B);
@@ -418,9 +470,9 @@ static void prove_jobs(xfg_ctx* c, std::vector<ProofJob>& jobs, const u64* trace
     const u64 rem_len = N >> (3 * nl) >> logbeta;  // D_final / blowup
     c->rem.ensure((size_t)B * std::max<u64>(rem_len, 1));
 
-    std::vector<AirConst> airs(B);
+    AirConst* airs = c->h_air.ensure(B);
     for (int b = 0; b < B; b++) airs[b] = jobs[b].air;
-    HIPCHK(hipMemcpyAsync(c->air.p, airs.data(), B * sizeof(AirConst), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->air.p, airs, B * sizeof(AirConst), hipMemcpyHostToDevice, s));
     // transcript seed: Context::to_elements || public inputs (ProverChannel::new)
     for (auto& j : jobs) {
         u64 e[20];
@@ -439,12 +491,12 @@ static void prove_jobs(xfg_ctx* c, std::vector<ProofJob>& jobs, const u64* trace
     stage_mark(c, 1);
     launch_leaves_lde(c->lde.p, 7, c->tnodes.p, 2 * N, B, logn, logbeta, s);
     launch_tree_top(c->tnodes.p, 2 * N, n / std::min<u64>(n, 256), B, s);
-    std::vector<Digest> roots;
+    Digest* roots = c->h_roots.ensure(B);
     stage_mark(c, 2);
     fetch_roots(c, c->tnodes.p, 2 * N, B, roots);
 
     // ---- 2. constraint composition coefficients (7 transition + 8 boundary)
-    std::vector<u64> co((size_t)B * 15);
+    u64* co = c->h_co.ensure((size_t)B * 15);
     for (int b = 0; b < B; b++) {
         auto& j = jobs[b];
         uint8_t rb[32];
@@ -454,7 +506,7 @@ static void prove_jobs(xfg_ctx* c, std::vector<ProofJob>& jobs, const u64* trace
         for (int k = 0; k < 15; k++)
             if (!j.coin.draw(co[(size_t)b * 15 + k])) j.status = XFG_PROVER_ERROR;
     }
-    HIPCHK(hipMemcpyAsync(c->coeffs.p, co.data(), co.size() * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->coeffs.p, co, (size_t)B * 15 * 8, hipMemcpyHostToDevice, s));
 
     // ---- 3. constraint evaluation + composition polynomial + commitment
     launch_constraint_eval(c->lde.p, c->air.p, c->coeffs.p, c->ce.p, logn, logbeta, T, B, s);
@@ -469,7 +521,7 @@ static void prove_jobs(xfg_ctx* c, std::vector<ProofJob>& jobs, const u64* trace
 
     // ---- 4. OOD point and frame
     const u64 g = gl_root(logn);
-    std::vector<u64> zp((size_t)B * 2);
+    u64* zp = c->h_zp.ensure((size_t)B * 2);
     for (int b = 0; b < B; b++) {
         auto& j = jobs[b];
         uint8_t rb[32];
@@ -481,15 +533,15 @@ static void prove_jobs(xfg_ctx* c, std::vector<ProofJob>& jobs, const u64* trace
         zp[2 * b] = z;
         zp[2 * b + 1] = gl_mul(z, g);
     }
-    HIPCHK(hipMemcpyAsync(c->zpts.p, zp.data(), zp.size() * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->zpts.p, zp, (size_t)B * 2 * 8, hipMemcpyHostToDevice, s));
     launch_ood(c->coef.p, c->hcoef.p, c->zpts.p, c->partial.p, c->ood.p, logn, B, s);
-    std::vector<u64> ood((size_t)B * 15);
-    HIPCHK(hipMemcpyAsync(ood.data(), c->ood.p, ood.size() * 8, hipMemcpyDeviceToHost, s));
+    u64* ood = c->h_ood.ensure((size_t)B * 15);
+    HIPCHK(hipMemcpyAsync(ood, c->ood.p, (size_t)B * 15 * 8, hipMemcpyDeviceToHost, s));
     stage_mark(c, 6);
     HIPCHK(hipStreamSynchronize(s));
 
     // ---- 5. DEEP composition polynomial (coefficient form) + its LDE
-    std::vector<DeepParams> dps(B);
+    DeepParams* dps = c->h_dp.ensure(B);
     for (int b = 0; b < B; b++) {
         auto& j = jobs[b];
         memcpy(j.ood, &ood[(size_t)b * 15], 15 * 8);
@@ -513,7 +565,7 @@ static void prove_jobs(xfg_ctx* c, std::vector<ProofJob>& jobs, const u64* trace
         P.c1 = c1;
         P.c2 = c2;
     }
-    HIPCHK(hipMemcpyAsync(c->dp.p, dps.data(), B * sizeof(DeepParams), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->dp.p, dps, B * sizeof(DeepParams), hipMemcpyHostToDevice, s));
     launch_deep(c->coef.p, c->hcoef.p, c->dp.p, c->bsum.p, c->carry.p, c->deep.p, logn, B, s);
     launch_lde(c->deep.p, n, c->f0.p, c->scratch.p, B, logn, logbeta, T, s);
     // degree check: deg(DEEP) == n - 2  <=>  coefficient n-2 != 0 (coefficient n-1 is 0 by construction)
@@ -521,7 +573,7 @@ static void prove_jobs(xfg_ctx* c, std::vector<ProofJob>& jobs, const u64* trace
     stage_mark(c, 7);
 
     // ---- 6. FRI layers (FriProver::build_layers), folding factor 8
-    std::vector<u64> alpha7h(B);
+    u64* alpha7h = c->h_a7.ensure(B);
     const u64 inv7 = gl_inv(GEN);
     for (unsigned l = 0; l < nl; l++) {
         const u64 rows = D[l] / 8;
@@ -541,22 +593,22 @@ static void prove_jobs(xfg_ctx* c, std::vector<ProofJob>& jobs, const u64* trace
             if (!j.coin.draw(a)) j.status = XFG_PROVER_ERROR;
             alpha7h[b] = gl_mul(a, inv7);
         }
-        HIPCHK(hipMemcpyAsync(c->alpha7.p, alpha7h.data(), B * 8, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(c->alpha7.p, alpha7h, B * 8, hipMemcpyHostToDevice, s));
         launch_fri_fold(src, sstride, cm, logn, logbeta, rows, (int)ilog2(D[l]), c->alpha7.p, c->flayer[l + 1].p,
                         rows, T, B, s);
     }
     // remainder: interpolate the last layer over 7*<w_D>, keep D/blowup coefficients
     // (with no folding layer this is the DEEP polynomial's own coefficients)
-    std::vector<u64> remh((size_t)B * rem_len);
+    u64* remh = c->h_rem.ensure((size_t)B * rem_len);
     if (nl > 0) {
         launch_interpolate(c->flayer[nl].p, D[nl], c->rem.p, rem_len, c->scratch.p, B, (int)ilog2(D[nl]), true,
                            rem_len, T, s);
-        HIPCHK(hipMemcpyAsync(remh.data(), c->rem.p, remh.size() * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(remh, c->rem.p, (size_t)B * rem_len * 8, hipMemcpyDeviceToHost, s));
     } else {
-        HIPCHK(hipMemcpy2DAsync(remh.data(), rem_len * 8, c->deep.p, n * 8, rem_len * 8, B, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpy2DAsync(remh, rem_len * 8, c->deep.p, n * 8, rem_len * 8, B, hipMemcpyDeviceToHost, s));
     }
-    std::vector<u64> dn2h(B);
-    HIPCHK(hipMemcpyAsync(dn2h.data(), c->dn2.p, B * 8, hipMemcpyDeviceToHost, s));
+    u64* dn2h = c->h_dn2.ensure(B);
+    HIPCHK(hipMemcpyAsync(dn2h, c->dn2.p, B * 8, hipMemcpyDeviceToHost, s));
     stage_mark(c, 8);
     HIPCHK(hipStreamSynchronize(s));
 
@@ -635,7 +687,9 @@ static void prove_jobs(xfg_ctx* c, std::vector<ProofJob>& jobs, const u64* trace
     c->gidx.ensure(allidx.size());
     c->gval.ensure(nvals);
     c->gdig.ensure(ndig);
-    HIPCHK(hipMemcpyAsync(c->gidx.p, allidx.data(), allidx.size() * 8, hipMemcpyHostToDevice, s));
+    u64* hidx = c->h_idx.ensure(allidx.size());
+    memcpy(hidx, allidx.data(), allidx.size() * 8);
+    HIPCHK(hipMemcpyAsync(c->gidx.p, hidx, allidx.size() * 8, hipMemcpyHostToDevice, s));
     {
         size_t vo = 0;
         const u64* vsrc[2] = {c->lde.p, c->hlde.p};
@@ -651,10 +705,10 @@ static void prove_jobs(xfg_ctx* c, std::vector<ProofJob>& jobs, const u64* trace
             dof += dseg[k].second;
         }
     }
-    std::vector<u64> gv(nvals);
-    std::vector<Digest> gd(ndig);
-    if (nvals) HIPCHK(hipMemcpyAsync(gv.data(), c->gval.p, nvals * 8, hipMemcpyDeviceToHost, s));
-    if (ndig) HIPCHK(hipMemcpyAsync(gd.data(), c->gdig.p, ndig * sizeof(Digest), hipMemcpyDeviceToHost, s));
+    u64* gv = c->h_gv.ensure(nvals);
+    Digest* gd = c->h_gd.ensure(ndig);
+    if (nvals) HIPCHK(hipMemcpyAsync(gv, c->gval.p, nvals * 8, hipMemcpyDeviceToHost, s));
+    if (ndig) HIPCHK(hipMemcpyAsync(gd, c->gdig.p, ndig * sizeof(Digest), hipMemcpyDeviceToHost, s));
     stage_mark(c, 9);
     HIPCHK(hipStreamSynchronize(s));
 
@@ -672,7 +726,8 @@ static void prove_jobs(xfg_ctx* c, std::vector<ProofJob>& jobs, const u64* trace
         p.u8(op.vecs.size());
         for (auto& v : op.vecs) {
             p.u8(v.size());
-            for (size_t k = 0; k < v.size(); k++) p.digest(gd[cursor++]);
+            p.put(&gd[cursor], 32 * v.size());
+            cursor += v.size();
         }
         w.u32(p.b.size());
         w.put(p.b.data(), p.b.size());
@@ -681,6 +736,7 @@ static void prove_jobs(xfg_ctx* c, std::vector<ProofJob>& jobs, const u64* trace
         auto& j = jobs[b];
         const u64 nu = j.pos.size();
         BW w;
+        w.b.reserve(j.commitments.size() + nu * 8 * (8 + 8 * nl) + (2 + nl) * nu * 32 * ilog2(N) + 1024);
         // Context
         w.u8(7); w.u8(0); w.u8(logn); w.u16(0);
         w.u8(8); w.u64_(P);
@@ -691,11 +747,13 @@ static void prove_jobs(xfg_ctx* c, std::vector<ProofJob>& jobs, const u64* trace
         // trace queries
         w.u8(1);
         w.u32(nu * 7 * 8);
-        for (u64 i = 0; i < nu * 7; i++) w.u64_(gv[cur_lde++]);
+        w.u64s(&gv[cur_lde], nu * 7);
+        cur_lde += nu * 7;
         write_paths(w, lay[b].ops[0], cur_t);
         // constraint queries
         w.u32(nu * 8);
-        for (u64 i = 0; i < nu; i++) w.u64_(gv[cur_h++]);
+        w.u64s(&gv[cur_h], nu);
+        cur_h += nu;
         write_paths(w, lay[b].ops[1], cur_hd);
         // OOD frame
         w.u16(1 + 14 * 8);
@@ -708,7 +766,8 @@ static void prove_jobs(xfg_ctx* c, std::vector<ProofJob>& jobs, const u64* trace
         for (unsigned l = 0; l < nl; l++) {
             u64 nk = lay[b].fpos[l].size();
             w.u32(nk * 8 * 8);
-            for (u64 i = 0; i < nk * 8; i++) w.u64_(gv[cur_fv[l]++]);
+            w.u64s(&gv[cur_fv[l]], nk * 8);
+            cur_fv[l] += nk * 8;
             write_paths(w, lay[b].ops[2 + l], cur_fd[l]);
         }
         w.u16(rem_len * 8);
@@ -726,6 +785,58 @@ static void prove_jobs(xfg_ctx* c, std::vector<ProofJob>& jobs, const u64* trace
         c->stage_ms[ST_HOST] =
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_host0).count();
     }
+}
+
+static Lane* lane0(xfg_ctx* c) {
+    if (c->lanes.empty()) {
+        c->lanes.emplace_back(new Lane());
+        HIPCHK(hipStreamCreateWithFlags(&c->lanes[0]->stream, hipStreamNonBlocking));
+        for (auto& e : c->lanes[0]->ev) HIPCHK(hipEventCreate(&e));
+    }
+    return c->lanes[0].get();
+}
+static void ensure_lanes(xfg_ctx* c, size_t k) {
+    lane0(c);
+    while (c->lanes.size() < k) {
+        c->lanes.emplace_back(new Lane());
+        HIPCHK(hipStreamCreateWithFlags(&c->lanes.back()->stream, hipStreamNonBlocking));
+        for (auto& e : c->lanes.back()->ev) HIPCHK(hipEventCreate(&e));
+    }
+}
+// proofs per lane below which a batch is not split (each lane runs a full pipeline)
+static const int MIN_PER_LANE = 8;
+static const int MAX_LANES = 2;
+
+static void prove_jobs(xfg_ctx* c, std::vector<ProofJob>& jobs, const u64* trace_host, u64 n, const Opts& o) {
+    const int B = (int)jobs.size();
+    ensure_tables(c, (int)(ilog2(n) + ilog2(o.beta)));
+    const Tables T = tables_of(c);
+    int nl = std::max(1, std::min(MAX_LANES, B / MIN_PER_LANE));
+    if (trace_host) nl = 1;
+    ensure_lanes(c, nl);
+    for (auto& L : c->lanes) L->timing = c->timing;
+    if (nl == 1) {
+        prove_lane(c->lanes[0].get(), T, jobs.data(), B, trace_host, n, o);
+        return;
+    }
+    std::vector<std::thread> th;
+    std::vector<std::exception_ptr> errs(nl);
+    int per = (B + nl - 1) / nl;
+    for (int l = 0; l < nl; l++) {
+        int b0 = l * per, b1 = std::min(B, b0 + per);
+        if (b0 >= b1) break;
+        th.emplace_back([&, l, b0, b1] {
+            try {
+                HIPCHK(hipSetDevice(c->device));
+                prove_lane(c->lanes[l].get(), T, jobs.data() + b0, b1 - b0, nullptr, n, o);
+            } catch (...) {
+                errs[l] = std::current_exception();
+            }
+        });
+    }
+    for (auto& t : th) t.join();
+    for (auto& e : errs)
+        if (e) std::rethrow_exception(e);
 }
 
 static int copy_out(xfg_ctx* c, const std::vector<uint8_t>& bytes, uint8_t* out, size_t* out_len) {
@@ -767,32 +878,27 @@ xfg_ctx* xfg_ctx_create(int device_id) {
     if (hipSetDevice(device_id) != hipSuccess) return nullptr;
     xfg_ctx* c = new xfg_ctx();
     c->device = device_id;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    try {
+        lane0(c);
+    } catch (...) {
         delete c;
         return nullptr;
     }
-    for (auto& e : c->ev) (void)hipEventCreate(&e);
     return c;
 }
 
 void xfg_ctx_destroy(xfg_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    (void)hipStreamSynchronize(c->stream);
-    c->air.release();
-    for (auto* b : {&c->coeffs, &c->trace, &c->coef, &c->scratch, &c->lde, &c->ce, &c->hcoef, &c->hlde, &c->zpts,
-                    &c->partial, &c->ood, &c->bsum, &c->carry, &c->deep, &c->f0, &c->alpha7, &c->rem, &c->gidx,
-                    &c->gval, &c->dn2})
-        b->release();
-    for (auto* b : {&c->tnodes, &c->hnodes, &c->gdig, &c->roots}) b->release();
-    c->dp.release();
-    for (auto& b : c->flayer) b.release();
-    for (auto& b : c->fnodes) b.release();
+    for (auto& L : c->lanes) {
+        (void)hipStreamSynchronize(L->stream);
+        L->release();
+        for (auto& e : L->ev) (void)hipEventDestroy(e);
+        (void)hipStreamDestroy(L->stream);
+    }
     c->tables.tw.release();
     c->tables.pow7.release();
     c->tables.ipow7.release();
-    for (auto& e : c->ev) (void)hipEventDestroy(e);
-    (void)hipStreamDestroy(c->stream);
     delete c;
 }
 
@@ -937,6 +1043,7 @@ int xfg_prove_burn_mint(xfg_ctx* c, const xfg_burn_inputs* in, uint64_t trace_le
 int xfg_set_timing(xfg_ctx* c, int enabled) {
     if (!c) return XFG_INVALID_ARGUMENT;
     c->timing = enabled != 0;
+    for (auto& L : c->lanes) L->timing = c->timing;
     return XFG_OK;
 }
 
@@ -944,7 +1051,7 @@ int xfg_stage_times(const xfg_ctx* c, double* ms, const char** names, int max) {
     if (!c) return 0;
     int k = std::min<int>(max, ST_COUNT);
     for (int i = 0; i < k; i++) {
-        if (ms) ms[i] = c->stage_ms[i];
+        if (ms) ms[i] = c->lanes.empty() ? 0.0 : c->lanes[0]->stage_ms[i];
         if (names) names[i] = STAGE_NAMES[i];
     }
     return k;
@@ -954,14 +1061,15 @@ int xfg_bench_lde(xfg_ctx* c, uint32_t count, uint64_t n, uint32_t blowup, uint3
     if (!c || !avg_ms || !is_pow2(n) || !is_pow2(blowup) || n < 8 || blowup < 2 || blowup > 16 || iters == 0)
         return XFG_INVALID_ARGUMENT;
     return guarded(c, [&]() -> int {
+        Lane* L = lane0(c);
         HIPCHK(hipSetDevice(c->device));
         const int logn = (int)ilog2(n), logbeta = (int)ilog2(blowup);
         const u64 N = n * blowup;
         ensure_tables(c, logn + logbeta);
         Tables T = tables_of(c);
-        c->coef.ensure((size_t)count * 7 * n);
-        c->scratch.ensure((size_t)count * 7 * N);
-        c->lde.ensure((size_t)count * 7 * N);
+        L->coef.ensure((size_t)count * 7 * n);
+        L->scratch.ensure((size_t)count * 7 * N);
+        L->lde.ensure((size_t)count * 7 * N);
         // deterministic canonical coefficients
         std::vector<u64> h((size_t)count * 7 * n);
         u64 x = 0x46472d535441524bULL;  // "FG-STARK"
@@ -972,15 +1080,15 @@ int xfg_bench_lde(xfg_ctx* c, uint32_t count, uint64_t n, uint32_t blowup, uint3
             z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
             v = (z ^ (z >> 31)) % P;
         }
-        HIPCHK(hipMemcpy(c->coef.p, h.data(), h.size() * 8, hipMemcpyHostToDevice));
-        launch_lde(c->coef.p, n, c->lde.p, c->scratch.p, count * 7, logn, logbeta, T, c->stream);  // warm
-        HIPCHK(hipEventRecord(c->ev[0], c->stream));
+        HIPCHK(hipMemcpy(L->coef.p, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+        launch_lde(L->coef.p, n, L->lde.p, L->scratch.p, count * 7, logn, logbeta, T, L->stream);  // warm
+        HIPCHK(hipEventRecord(L->ev[0], L->stream));
         for (uint32_t i = 0; i < iters; i++)
-            launch_lde(c->coef.p, n, c->lde.p, c->scratch.p, count * 7, logn, logbeta, T, c->stream);
-        HIPCHK(hipEventRecord(c->ev[1], c->stream));
-        HIPCHK(hipEventSynchronize(c->ev[1]));
+            launch_lde(L->coef.p, n, L->lde.p, L->scratch.p, count * 7, logn, logbeta, T, L->stream);
+        HIPCHK(hipEventRecord(L->ev[1], L->stream));
+        HIPCHK(hipEventSynchronize(L->ev[1]));
         float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+        HIPCHK(hipEventElapsedTime(&ms, L->ev[0], L->ev[1]));
         *avg_ms = ms / iters;
         return XFG_OK;
     });
@@ -990,19 +1098,20 @@ int xfg_debug_lde(xfg_ctx* c, const uint64_t* coef, uint32_t npoly, uint64_t n, 
     if (!c || !coef || !out || !is_pow2(n) || !is_pow2(blowup) || n < 8 || blowup < 2 || blowup > 16)
         return XFG_INVALID_ARGUMENT;
     return guarded(c, [&]() -> int {
+        Lane* L = lane0(c);
         HIPCHK(hipSetDevice(c->device));
         const int logn = (int)ilog2(n), logbeta = (int)ilog2(blowup);
         const u64 N = n * blowup;
         ensure_tables(c, logn + logbeta);
         Tables T = tables_of(c);
-        c->coef.ensure((size_t)npoly * n);
-        c->scratch.ensure((size_t)npoly * N);
-        c->lde.ensure((size_t)npoly * N);
-        HIPCHK(hipMemcpy(c->coef.p, coef, (size_t)npoly * n * 8, hipMemcpyHostToDevice));
-        launch_lde(c->coef.p, n, c->lde.p, c->scratch.p, npoly, logn, logbeta, T, c->stream);
+        L->coef.ensure((size_t)npoly * n);
+        L->scratch.ensure((size_t)npoly * N);
+        L->lde.ensure((size_t)npoly * N);
+        HIPCHK(hipMemcpy(L->coef.p, coef, (size_t)npoly * n * 8, hipMemcpyHostToDevice));
+        launch_lde(L->coef.p, n, L->lde.p, L->scratch.p, npoly, logn, logbeta, T, L->stream);
         std::vector<u64> cm((size_t)npoly * N);
-        HIPCHK(hipMemcpyAsync(cm.data(), c->lde.p, cm.size() * 8, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipMemcpyAsync(cm.data(), L->lde.p, cm.size() * 8, hipMemcpyDeviceToHost, L->stream));
+        HIPCHK(hipStreamSynchronize(L->stream));
         for (u64 p = 0; p < npoly; p++)  // coset-major -> natural order
             for (u64 t = 0; t < blowup; t++)
                 for (u64 m = 0; m < n; m++) out[p * N + t + blowup * m] = cm[(p * blowup + t) * n + m];
@@ -1013,17 +1122,18 @@ int xfg_debug_lde(xfg_ctx* c, const uint64_t* coef, uint32_t npoly, uint64_t n, 
 int xfg_debug_interpolate(xfg_ctx* c, const uint64_t* evals, uint32_t npoly, uint64_t n, int offset7, uint64_t* out) {
     if (!c || !evals || !out || !is_pow2(n) || n < 8) return XFG_INVALID_ARGUMENT;
     return guarded(c, [&]() -> int {
+        Lane* L = lane0(c);
         HIPCHK(hipSetDevice(c->device));
         const int logn = (int)ilog2(n);
         ensure_tables(c, std::max(logn, c->tables.LM));
         Tables T = tables_of(c);
-        c->trace.ensure((size_t)npoly * n);
-        c->coef.ensure((size_t)npoly * n);
-        c->scratch.ensure((size_t)npoly * n);
-        HIPCHK(hipMemcpy(c->trace.p, evals, (size_t)npoly * n * 8, hipMemcpyHostToDevice));
-        launch_interpolate(c->trace.p, n, c->coef.p, n, c->scratch.p, npoly, logn, offset7 != 0, n, T, c->stream);
-        HIPCHK(hipMemcpyAsync(out, c->coef.p, (size_t)npoly * n * 8, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
+        L->trace.ensure((size_t)npoly * n);
+        L->coef.ensure((size_t)npoly * n);
+        L->scratch.ensure((size_t)npoly * n);
+        HIPCHK(hipMemcpy(L->trace.p, evals, (size_t)npoly * n * 8, hipMemcpyHostToDevice));
+        launch_interpolate(L->trace.p, n, L->coef.p, n, L->scratch.p, npoly, logn, offset7 != 0, n, T, L->stream);
+        HIPCHK(hipMemcpyAsync(out, L->coef.p, (size_t)npoly * n * 8, hipMemcpyDeviceToHost, L->stream));
+        HIPCHK(hipStreamSynchronize(L->stream));
         return XFG_OK;
     });
 }

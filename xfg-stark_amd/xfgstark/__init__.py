@@ -247,8 +247,10 @@ class XfgBurnMintProver:
             arr[i] = s
         o = self._options._c()
         cap = _lib.xfg_proof_size_bound(trace_length, C.byref(o))
-        big = C.create_string_buffer(cap * k)
-        base = C.addressof(big)
+        if getattr(self, "_out_cap", 0) < cap * k:
+            self._out = C.create_string_buffer(cap * k)
+            self._out_cap = cap * k
+        base = C.addressof(self._out)
         outs = (_u8p * k)(*[C.cast(base + i * cap, _u8p) for i in range(k)])
         lens = (C.c_size_t * k)(*([cap] * k))
         sts = (C.c_int * k)()
