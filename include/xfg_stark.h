@@ -103,6 +103,8 @@ int xfg_prove_batch(xfg_ctx* ctx, uint32_t count, const xfg_burn_inputs* inputs,
 int xfg_burn_air_consts(const xfg_burn_inputs* in, xfg_air_consts* out);
 
 /* ---- instrumentation (benchmarks / parity tests) ---- */
+/* host-side field arithmetic of the library (mul, add, sub) for self-tests; canonical inputs */
+int xfg_selftest_field(uint64_t a, uint64_t b, uint64_t* out3);
 /* per-stage device milliseconds of the last prove call when timing is enabled (returns count) */
 int xfg_set_timing(xfg_ctx* ctx, int enabled);
 int xfg_stage_times(const xfg_ctx* ctx, double* ms, const char** names, int max);

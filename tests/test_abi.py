@@ -94,3 +94,17 @@ def test_no_gpu_means_loud_failure():
         pytest.skip("GPU present")
     with pytest.raises(xfgstark.XfgStarkError):
         xfgstark.XfgBurnMintProver()
+
+
+def test_host_field_arithmetic():
+    import random
+    import xfgstark
+    lib = C.CDLL(xfgstark.LIB_PATH)
+    P = 0xFFFFFFFF00000001
+    out = (C.c_uint64 * 3)()
+    rng = random.Random(5)
+    edge = [0, 1, 2, P - 1, P - 2, 2**32 - 1, 2**32, 2**32 + 1, 2**63, P - 2**32]
+    pairs = [(a, b) for a in edge for b in edge] + [(rng.randrange(P), rng.randrange(P)) for _ in range(3000)]
+    for a, b in pairs:
+        assert lib.xfg_selftest_field(C.c_uint64(a), C.c_uint64(b), out) == 0
+        assert list(out) == [a * b % P, (a + b) % P, (a - b) % P], (a, b)

@@ -28,149 +28,6 @@ __device__ __forceinline__ u64 tw_ipow(const Tables& T, int k, u64 e) {
     return T.tw[(M - ((e << (T.LM - k)) & (M - 1))) & (M - 1)];
 }
 
-// ============================================================================ NTT
-struct NttArgs {
-    const u64* in;
-    u64* y;
-    u64* out;
-    u64 in_stride, out_stride;
-    int logn, logR, logC, logTC, logTR;
-    int logbeta;  // forward: number of cosets = 2^logbeta
-    int inverse;
-    int off7;
-    u64 scale;
-    u64 keep;
-    Tables T;
-};
-
-// radix-2 DIT stages over `nseq` sequences of length 2^logS stored as rows of `tile` (row pitch
-// S+1, inputs already in bit-reversed positions); ltw[i] = w_S^{+-i}, i < S/2
-__device__ __forceinline__ void lds_dit(u64* tile, const u64* ltw, int logS, int nseq) {
-    const int S = 1 << logS, pitch = S + 1, half = S >> 1;
-    const int nb = nseq * half;
-    for (int s = 0; s < logS; s++) {
-        const int h = 1 << s;
-        for (int b = threadIdx.x; b < nb; b += blockDim.x) {
-            int seq = b >> (logS - 1), bi = b & (half - 1);
-            int pos = bi & (h - 1), i0 = ((bi >> s) << (s + 1)) + pos;
-            u64* row = tile + seq * pitch;
-            u64 w = ltw[pos << (logS - 1 - s)];
-            u64 u = row[i0], v = gl_mul(row[i0 + h], w);
-            row[i0] = gl_add(u, v);
-            row[i0 + h] = gl_sub(u, v);
-        }
-        __syncthreads();
-    }
-}
-
-__global__ __launch_bounds__(256) void ntt_cols_kernel(NttArgs a) {
-    extern __shared__ u64 lds[];
-    const int R = 1 << a.logR, TC = 1 << a.logTC;
-    const u64 n = 1ULL << a.logn;
-    const int poly = blockIdx.y, col0 = blockIdx.x * TC;
-    u64* tile = lds;
-    u64* ltw = lds + TC * (R + 1);
-    for (int i = threadIdx.x; i < R / 2; i += blockDim.x)
-        ltw[i] = a.inverse ? tw_ipow(a.T, a.logR, i) : tw_pow(a.T, a.logR, i);
-    const int nelem = R * TC;
-    const u64* in = a.in + (u64)poly * a.in_stride;
-    const int ncos = a.inverse ? 1 : (1 << a.logbeta);
-    const int logN = a.logn + a.logbeta;
-    for (int t = 0; t < ncos; t++) {
-        for (int e = threadIdx.x; e < nelem; e += blockDim.x) {
-            int j1 = e >> a.logTC, jj = e & (TC - 1);
-            u64 j = ((u64)j1 << a.logC) + col0 + jj;
-            u64 v = in[j];
-            if (!a.inverse) {
-                // coset shift (7 w_N^t)^j folded into the load
-                v = gl_mul(v, a.T.pow7[j]);
-                if (t) v = gl_mul(v, tw_pow(a.T, logN, ((u64)t * j) & ((1ULL << logN) - 1)));
-            }
-            tile[jj * (R + 1) + brev(j1, a.logR)] = v;
-        }
-        __syncthreads();
-        lds_dit(tile, ltw, a.logR, TC);
-        u64* y = a.y + ((u64)poly * ncos + t) * n;
-        for (int e = threadIdx.x; e < nelem; e += blockDim.x) {
-            int k1 = e >> a.logTC, jj = e & (TC - 1);
-            u64 j2 = col0 + jj;
-            u64 ex = (j2 * (u64)k1) & (n - 1);
-            u64 w = a.inverse ? tw_ipow(a.T, a.logn, ex) : tw_pow(a.T, a.logn, ex);
-            y[((u64)k1 << a.logC) + j2] = gl_mul(tile[jj * (R + 1) + k1], w);
-        }
-        __syncthreads();
-    }
-}
-
-__global__ __launch_bounds__(256) void ntt_rows_kernel(NttArgs a) {
-    extern __shared__ u64 lds[];
-    const int C = 1 << a.logC, TR = 1 << a.logTR;
-    const u64 n = 1ULL << a.logn;
-    const int pt = blockIdx.y, k10 = blockIdx.x * TR;
-    u64* tile = lds;
-    u64* ltw = lds + TR * (C + 1);
-    for (int i = threadIdx.x; i < C / 2; i += blockDim.x)
-        ltw[i] = a.inverse ? tw_ipow(a.T, a.logC, i) : tw_pow(a.T, a.logC, i);
-    const int nelem = TR * C;
-    const u64* y = a.y + (u64)pt * n;
-    for (int e = threadIdx.x; e < nelem; e += blockDim.x) {
-        int r = e >> a.logC, j2 = e & (C - 1);
-        tile[r * (C + 1) + brev(j2, a.logC)] = y[((u64)(k10 + r) << a.logC) + j2];
-    }
-    __syncthreads();
-    lds_dit(tile, ltw, a.logC, TR);
-    for (int e = threadIdx.x; e < nelem; e += blockDim.x) {
-        int k2 = e >> a.logTR, r = e & (TR - 1);
-        u64 k = (u64)(k10 + r) + ((u64)k2 << a.logR);
-        u64 v = tile[r * (C + 1) + k2];
-        if (a.inverse) {
-            if (k >= a.keep) continue;
-            v = gl_mul(v, a.scale);
-            if (a.off7) v = gl_mul(v, a.T.ipow7[k]);
-            a.out[(u64)pt * a.out_stride + k] = v;
-        } else {
-            a.out[(u64)pt * n + k] = v;  // pt = poly * beta + t  -> coset-major
-        }
-    }
-}
-
-static void ntt_plan(NttArgs& a, int logn) {
-    a.logn = logn;
-    a.logR = logn / 2;
-    a.logC = logn - a.logR;
-    a.logTC = a.logC < 12 - a.logR ? a.logC : 12 - a.logR;
-    a.logTR = a.logR < 12 - a.logC ? a.logR : 12 - a.logC;
-    if (a.logTC < 0) a.logTC = 0;
-    if (a.logTR < 0) a.logTR = 0;
-}
-static void ntt_run(NttArgs& a, int npoly, int ncos, hipStream_t s) {
-    const int R = 1 << a.logR, C = 1 << a.logC;
-    size_t lds1 = ((size_t)(1 << a.logTC) * (R + 1) + R / 2) * sizeof(u64);
-    size_t lds2 = ((size_t)(1 << a.logTR) * (C + 1) + C / 2) * sizeof(u64);
-    dim3 g1(C >> a.logTC, npoly), g2(R >> a.logTR, npoly * ncos);
-    hipLaunchKernelGGL(ntt_cols_kernel, g1, dim3(256), lds1, s, a);
-    hipLaunchKernelGGL(ntt_rows_kernel, g2, dim3(256), lds2, s, a);
-    XFG_CHECK_LAUNCH();
-}
-
-void launch_lde(const u64* coef, u64 coef_stride, u64* out, u64* scratch, int npoly, int logn, int logbeta,
-                const Tables& T, hipStream_t s) {
-    NttArgs a{};
-    ntt_plan(a, logn);
-    a.in = coef; a.in_stride = coef_stride; a.y = scratch; a.out = out;
-    a.logbeta = logbeta; a.inverse = 0; a.T = T;
-    ntt_run(a, npoly, 1 << logbeta, s);
-}
-void launch_interpolate(const u64* evals, u64 in_stride, u64* out, u64 out_stride, u64* scratch, int npoly, int logn,
-                        bool off7, u64 keep, const Tables& T, hipStream_t s) {
-    NttArgs a{};
-    ntt_plan(a, logn);
-    a.in = evals; a.in_stride = in_stride; a.y = scratch; a.out = out; a.out_stride = out_stride;
-    a.logbeta = 0; a.inverse = 1; a.off7 = off7 ? 1 : 0; a.keep = keep; a.T = T;
-    a.scale = gl_inv(1ULL << logn);
-    ntt_run(a, npoly, 1, s);
-}
-
 // ============================================================================ Merkle
 // builds `levels` levels above the per-thread nodes held in lds[0..nthreads) and writes them;
 // node index of thread i at the base level is base_idx + i

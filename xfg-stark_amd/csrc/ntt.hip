@@ -1,0 +1,354 @@
+// Four-step Goldilocks NTT for CDNA4 (gfx950): coset LDE and (coset) interpolation.
+//
+// Replaces winter-math fft::interpolate_poly / evaluate_poly_with_offset as used by Winterfell's
+// DefaultTraceLde, CompositionPoly and DeepCompositionPoly (the LDE behind
+// src/burn_mint_air.rs:504-514 `new_trace_lde`).
+//
+// n = R * C. Pass A: size-R DFTs down the columns of the [R][C] view, pass B: size-C DFTs
+// along the rows. Each pass is a chain of Stockham autosort steps with radix-16 butterflies in
+// registers (16 elements per thread, 256 threads, 4096-element tiles):
+//   * the first step of a pass loads straight from HBM (coalesced: 16 lanes cover 128 B),
+//   * the middle steps go through one padded LDS tile,
+//   * the last step stores straight to HBM, applying the four-step / coset twiddles as running
+//     products (2 table reads per thread, no per-element twiddle-table gathers).
+// Twiddles inside a radix-16 butterfly are 16th roots of unity = powers of two in Goldilocks
+// (w_16 = 2^156, w_8 = 2^120, w_4 = 2^48, w_2 = 2^96 = -1): shifts + one reduction.
+//
+// Forward LDE output is coset-major: out[p][t][m] = P(7 * w_N^(t + beta*m)), N = beta * n.
+// The coset shift (7 w_N^t)^j, j = C j1 + j2, is split into a pre-factor 7^(C j1) w_(beta R)^(t j1)
+// (LDS table per coset) and a post-factor 7^j2 w_N^(j2 t) folded into the four-step twiddle.
+#include "kernels.hpp"
+
+namespace xfg {
+
+// ---------------------------------------------------------------- shift-based multiplies
+// x * 2^s mod p for 0 <= s < 192 (2^96 == -1); s is a compile-time constant after unrolling
+__device__ __forceinline__ u64 mul_pow2(u64 x, int s) {
+    bool neg = s >= 96;
+    if (neg) s -= 96;
+    u64 r;
+    if (s == 0) r = x;
+    else if (s < 64) r = gl_reduce(x >> (64 - s), x << s);
+    else {
+        u64 y = gl_reduce(x >> (96 - s), x << (s - 32));
+        r = gl_reduce(y >> 32, y << 32);
+    }
+    return neg ? gl_neg(r) : r;
+}
+// exponent of two of w_{2^k} (Winterfell's roots: get_root_of_unity(k))
+__host__ __device__ constexpr int root_exp2(int k) {
+    return k == 1 ? 96 : k == 2 ? 48 : k == 3 ? 120 : k == 4 ? 156 : 0;
+}
+__host__ __device__ constexpr int brev_c(int x, int bits) {
+    int r = 0;
+    for (int i = 0; i < bits; i++) r |= ((x >> i) & 1) << (bits - 1 - i);
+    return r;
+}
+
+// in-register DFT of size 2^LOGR (<= 16): v[q] <- sum_r v[r] w_R^(+-rq), natural order in/out
+template <int LOGR, bool INV>
+__device__ __forceinline__ void dft_reg(u64* v) {
+    constexpr int R = 1 << LOGR;
+    u64 a[R];
+#pragma unroll
+    for (int i = 0; i < R; i++) a[i] = v[brev_c(i, LOGR)];
+#pragma unroll
+    for (int s = 0; s < LOGR; s++) {
+        const int h = 1 << s;
+#pragma unroll
+        for (int b = 0; b < R / 2; b++) {
+            const int pos = b & (h - 1), i0 = ((b >> s) << (s + 1)) + pos;
+            int e = (root_exp2(s + 1) * pos) % 192;
+            if (INV && e) e = 192 - e;
+            u64 t = mul_pow2(a[i0 + h], e);
+            u64 u = a[i0];
+            a[i0] = gl_add(u, t);
+            a[i0 + h] = gl_sub(u, t);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < R; i++) v[i] = a[i];
+}
+
+constexpr int THREADS = 256;
+// LDS tile: row `seq` of length S at seq * PITCH; element i at i + (i >> 4). The pad word per 16
+// elements makes the stride-16 stores of a first step conflict-free; the odd pitch does the same
+// for lanes walking across rows.
+__host__ __device__ constexpr int row_pitch(int S) { return S + S / 16 + 1; }
+__device__ __forceinline__ int phys(int i) { return i + (i >> 4); }
+
+__device__ __forceinline__ u64 tw_get(const Tables& T, int k, u64 e, bool inv) {
+    const u64 M = 1ULL << T.LM;
+    u64 idx = (e << (T.LM - k)) & (M - 1);
+    if (inv) idx = (M - idx) & (M - 1);
+    return T.tw[idx];
+}
+
+// ---------------------------------------------------------------- one Stockham step
+// Radix 2^LOGR step of a size-2^LOGS DFT on 2^lognseq sequences. Group g of the step is
+// (seq, j); SEQ_FAST maps consecutive lanes to consecutive sequences, otherwise to consecutive j.
+// ld(seq, i) reads logical element i of a sequence; st(seq, base, stride, v) receives the R
+// outputs of a group, which belong at logical positions base + r * stride.
+// IN_PLACE: every load of the step completes (barrier) before any store.
+template <int LOGS, int LOGR, bool INV, bool SEQ_FAST, bool IN_PLACE, class LD, class ST>
+__device__ __forceinline__ void stockham(int lognseq, int Ns, const u64* ltw, LD ld, ST st) {
+    constexpr int S = 1 << LOGS, R = 1 << LOGR, G = S / R, PER = 16 / R;
+    const int nseq = 1 << lognseq;
+    const int groups = nseq * G;
+    u64 v[PER][R];
+    int gs[PER], gj[PER];
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int g = threadIdx.x + THREADS * q;
+        gs[q] = -1;
+        gj[q] = 0;
+        if (g < groups) {
+            const int seq = SEQ_FAST ? (g & (nseq - 1)) : (g / G);
+            const int j = SEQ_FAST ? (g >> lognseq) : (g % G);
+#pragma unroll
+            for (int r = 0; r < R; r++) v[q][r] = ld(seq, j + r * G);
+            if (Ns > 1) {
+                const int k = j % Ns, step = S / (Ns * R);
+#pragma unroll
+                for (int r = 1; r < R; r++) v[q][r] = gl_mul(v[q][r], ltw[r * k * step]);
+            }
+            dft_reg<LOGR, INV>(v[q]);
+            gs[q] = seq;
+            gj[q] = j;
+        }
+    }
+    if (IN_PLACE) __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        if (gs[q] >= 0) {
+            const int j = gj[q];
+            st(gs[q], (j / Ns) * Ns * R + (j % Ns), Ns, v[q]);
+        }
+    }
+}
+
+// steps of a size-2^LOGS DFT: the remainder radix first, then radix 16
+template <int LOGS>
+struct Plan {
+    static constexpr int REM = LOGS % 4;
+    static constexpr int NSTEP = LOGS / 4 + (REM ? 1 : 0);
+    static constexpr int FIRST_LOGR = REM ? REM : 4;
+    // radix of the step that produces the final outputs
+    static constexpr int LAST_R = NSTEP == 1 ? (1 << FIRST_LOGR) : 16;
+};
+
+// Whole DFT of every sequence: the first step loads with ldg (global), middle steps run in the
+// LDS tile, the last step stores with stg (global). A one-step DFT goes global -> global.
+template <int LOGS, bool INV, bool FIRST_SEQ_FAST, class LDG, class STG>
+__device__ __forceinline__ void pass_dft(u64* tile, int lognseq, const u64* ltw, LDG ldg, STG stg) {
+    using PL = Plan<LOGS>;
+    constexpr int PITCH = row_pitch(1 << LOGS);
+    if constexpr (PL::NSTEP == 1) {
+        stockham<LOGS, PL::FIRST_LOGR, INV, FIRST_SEQ_FAST, false>(lognseq, 1, ltw, ldg, stg);
+    } else {
+        stockham<LOGS, PL::FIRST_LOGR, INV, FIRST_SEQ_FAST, false>(
+            lognseq, 1, ltw, ldg, [&](int seq, int base, int stride, u64* v) {
+                u64* row = tile + seq * PITCH;
+#pragma unroll
+                for (int r = 0; r < (1 << PL::FIRST_LOGR); r++) row[phys(base + r * stride)] = v[r];
+            });
+        __syncthreads();
+        int Ns = 1 << PL::FIRST_LOGR;
+#pragma unroll
+        for (int st = 1; st < PL::NSTEP - 1; st++) {
+            stockham<LOGS, 4, INV, true, true>(
+                lognseq, Ns, ltw, [&](int seq, int i) { return tile[seq * PITCH + phys(i)]; },
+                [&](int seq, int base, int stride, u64* v) {
+                    u64* row = tile + seq * PITCH;
+#pragma unroll
+                    for (int r = 0; r < 16; r++) row[phys(base + r * stride)] = v[r];
+                });
+            __syncthreads();
+            Ns <<= 4;
+        }
+        stockham<LOGS, 4, INV, true, false>(lognseq, Ns, ltw,
+                                            [&](int seq, int i) { return tile[seq * PITCH + phys(i)]; }, stg);
+        __syncthreads();
+    }
+}
+
+struct NttArgs {
+    const u64* in;
+    u64* y;
+    u64* out;
+    u64 in_stride, out_stride;
+    int logn, logR, logC;
+    int logbeta;  // forward: 2^logbeta cosets
+    int off7;     // inverse: scale coefficient k by 7^-k
+    u64 scale;    // inverse: n^-1
+    u64 keep;     // inverse: coefficients written
+    Tables T;
+};
+
+// ---------------------------------------------------------------- pass A: column DFTs (size R)
+// forward, coset t: x[j1] = c[C j1 + j2] * 7^(C j1) w_(beta R)^(t j1)
+//   y[t][k1][j2] = X[k1] * 7^j2 * w_N^(j2 (t + beta k1))
+// inverse: y[k1][j2] = X[k1] * w_n^-(j2 k1)
+template <int LOGR, bool INV>
+__global__ __launch_bounds__(THREADS) void ntt_pass_a(NttArgs a) {
+    constexpr int R = 1 << LOGR, PITCH = row_pitch(R), RR = Plan<LOGR>::LAST_R;
+    extern __shared__ u64 lds[];
+    const int logTC = (a.logC < 12 - LOGR) ? a.logC : 12 - LOGR;
+    const int TC = 1 << logTC;
+    u64* tile = lds;
+    u64* ltw = lds + TC * PITCH;
+    u64* pre = ltw + R;  // forward: 7^(C j1) w_(beta R)^(t j1) for the current coset
+    const int poly = blockIdx.y, col0 = blockIdx.x * TC;
+    const u64 n = 1ULL << a.logn;
+    const int logN = a.logn + a.logbeta;
+    const u64 maskN = (1ULL << logN) - 1;
+    for (int i = threadIdx.x; i < R; i += THREADS) {
+        ltw[i] = tw_get(a.T, LOGR, i, INV);
+        if (!INV) pre[i] = a.T.pow7[(u64)i << a.logC];
+    }
+    __syncthreads();
+    const u64* in = a.in + (u64)poly * a.in_stride;
+    const int ncos = INV ? 1 : (1 << a.logbeta);
+    for (int t = 0; t < ncos; t++) {
+        if (!INV && t > 0) {
+            // advance pre[j1] from coset t-1 to t: * w_(beta R)^(j1)
+            for (int i = threadIdx.x; i < R; i += THREADS)
+                pre[i] = gl_mul(pre[i], tw_get(a.T, LOGR + a.logbeta, i, false));
+            __syncthreads();
+        }
+        u64* y = a.y + ((u64)poly * ncos + t) * n;
+        auto ldg = [&](int seq, int j1) -> u64 {
+            u64 v = in[((u64)j1 << a.logC) + col0 + seq];
+            return INV ? v : gl_mul(v, pre[j1]);
+        };
+        auto stg = [&](int seq, int base, int stride, u64* v) {
+            const u64 j2 = col0 + seq;
+            u64 w, step;
+            if (INV) {
+                w = tw_get(a.T, a.logn, (j2 * (u64)base) & (n - 1), true);
+                step = tw_get(a.T, a.logn, (j2 * (u64)stride) & (n - 1), true);
+            } else {
+                // 7^j2 w_N^(j2 (t + beta base)); step w_N^(j2 beta stride) = w_n^(j2 stride)
+                w = gl_mul(a.T.pow7[j2],
+                           tw_get(a.T, logN, (j2 * ((u64)t + ((u64)base << a.logbeta))) & maskN, false));
+                step = tw_get(a.T, a.logn, (j2 * (u64)stride) & (n - 1), false);
+            }
+#pragma unroll
+            for (int r = 0; r < RR; r++) {
+                y[((u64)(base + r * stride) << a.logC) + j2] = gl_mul(v[r], w);
+                if (r + 1 < RR) w = gl_mul(w, step);
+            }
+        };
+        pass_dft<LOGR, INV, true>(tile, logTC, ltw, ldg, stg);
+    }
+}
+
+// ---------------------------------------------------------------- pass B: row DFTs (size C)
+template <int LOGC, bool INV>
+__global__ __launch_bounds__(THREADS) void ntt_pass_b(NttArgs a) {
+    constexpr int C = 1 << LOGC, RR = Plan<LOGC>::LAST_R;
+    extern __shared__ u64 lds[];
+    const int logTR = (a.logR < 12 - LOGC) ? a.logR : 12 - LOGC;
+    const int TR = 1 << logTR;
+    u64* tile = lds;
+    u64* ltw = lds + TR * row_pitch(C);
+    const int pt = blockIdx.y, k10 = blockIdx.x * TR;
+    const u64 n = 1ULL << a.logn;
+    for (int i = threadIdx.x; i < C; i += THREADS) ltw[i] = tw_get(a.T, LOGC, i, INV);
+    __syncthreads();
+    const u64* y = a.y + (u64)pt * n;
+    auto ldg = [&](int seq, int j2) -> u64 { return y[((u64)(k10 + seq) << LOGC) + j2]; };
+    auto stg = [&](int seq, int base, int stride, u64* v) {
+#pragma unroll
+        for (int r = 0; r < RR; r++) {
+            const u64 k = (u64)(k10 + seq) + ((u64)(base + r * stride) << a.logR);
+            if (INV) {
+                if (k < a.keep) {
+                    u64 x = gl_mul(v[r], a.scale);
+                    if (a.off7) x = gl_mul(x, a.T.ipow7[k]);
+                    a.out[(u64)pt * a.out_stride + k] = x;
+                }
+            } else {
+                a.out[(u64)pt * n + k] = v[r];  // pt = poly * beta + t -> coset-major
+            }
+        }
+    };
+    // multi-step rows: first step along the row (coalesced loads); one-step rows: lanes along
+    // sequences so the (final) global store is coalesced
+    pass_dft<LOGC, INV, (Plan<LOGC>::NSTEP == 1)>(tile, logTR, ltw, ldg, stg);
+}
+
+// ---------------------------------------------------------------- dispatch
+template <bool INV>
+static void run_pass_a(int logR, dim3 g, size_t lds, hipStream_t s, const NttArgs& a) {
+#define XFG_CASE_A(L) \
+    case L: hipLaunchKernelGGL((ntt_pass_a<L, INV>), g, dim3(THREADS), lds, s, a); break;
+    switch (logR) {
+        XFG_CASE_A(1) XFG_CASE_A(2) XFG_CASE_A(3) XFG_CASE_A(4) XFG_CASE_A(5) XFG_CASE_A(6)
+        XFG_CASE_A(7) XFG_CASE_A(8) XFG_CASE_A(9) XFG_CASE_A(10)
+        default: break;
+    }
+#undef XFG_CASE_A
+}
+template <bool INV>
+static void run_pass_b(int logC, dim3 g, size_t lds, hipStream_t s, const NttArgs& a) {
+#define XFG_CASE_B(L) \
+    case L: hipLaunchKernelGGL((ntt_pass_b<L, INV>), g, dim3(THREADS), lds, s, a); break;
+    switch (logC) {
+        XFG_CASE_B(2) XFG_CASE_B(3) XFG_CASE_B(4) XFG_CASE_B(5) XFG_CASE_B(6) XFG_CASE_B(7)
+        XFG_CASE_B(8) XFG_CASE_B(9) XFG_CASE_B(10) XFG_CASE_B(11)
+        default: break;
+    }
+#undef XFG_CASE_B
+}
+
+static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
+    a.logR = a.logn / 2;
+    a.logC = a.logn - a.logR;
+    const int R = 1 << a.logR, C = 1 << a.logC;
+    const int logTC = a.logC < 12 - a.logR ? a.logC : 12 - a.logR;
+    const int logTR = a.logR < 12 - a.logC ? a.logR : 12 - a.logC;
+    const int ncos = inv ? 1 : (1 << a.logbeta);
+    size_t lds_a = ((size_t)(1 << logTC) * row_pitch(R) + 2 * R) * sizeof(u64);
+    size_t lds_b = ((size_t)(1 << logTR) * row_pitch(C) + C) * sizeof(u64);
+    dim3 ga(C >> logTC, npoly), gb(R >> logTR, npoly * ncos);
+    if (inv) {
+        run_pass_a<true>(a.logR, ga, lds_a, s, a);
+        run_pass_b<true>(a.logC, gb, lds_b, s, a);
+    } else {
+        run_pass_a<false>(a.logR, ga, lds_a, s, a);
+        run_pass_b<false>(a.logC, gb, lds_b, s, a);
+    }
+}
+
+void launch_lde(const u64* coef, u64 coef_stride, u64* out, u64* scratch, int npoly, int logn, int logbeta,
+                const Tables& T, hipStream_t s) {
+    NttArgs a{};
+    a.in = coef;
+    a.in_stride = coef_stride;
+    a.y = scratch;
+    a.out = out;
+    a.logn = logn;
+    a.logbeta = logbeta;
+    a.T = T;
+    ntt_run(a, npoly, false, s);
+}
+
+void launch_interpolate(const u64* evals, u64 in_stride, u64* out, u64 out_stride, u64* scratch, int npoly, int logn,
+                        bool off7, u64 keep, const Tables& T, hipStream_t s) {
+    NttArgs a{};
+    a.in = evals;
+    a.in_stride = in_stride;
+    a.y = scratch;
+    a.out = out;
+    a.out_stride = out_stride;
+    a.logn = logn;
+    a.logbeta = 0;
+    a.off7 = off7 ? 1 : 0;
+    a.keep = keep;
+    a.T = T;
+    a.scale = gl_inv(1ULL << logn);
+    ntt_run(a, npoly, true, s);
+}
+
+}  // namespace xfg

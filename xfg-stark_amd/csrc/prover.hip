@@ -51,7 +51,7 @@ static Opts to_opts(const xfg_options* o) {
 // ProofOptions::new validation (winter-air 0.8) + what this GPU path implements
 static const char* check_options(u64 n, const Opts& o) {
     if (!is_pow2(n) || n < 8) return "trace length must be a power of two and at least 8";
-    if (n > (1ULL << 22)) return "trace length above 2^22 is not supported";
+    if (n > (1ULL << 21)) return "trace length above 2^21 is not supported";
     if (!is_pow2(o.beta) || o.beta < 2 || o.beta > 16) return "blowup factor must be a power of two in [2, 16]";
     if (o.q < 1 || o.q > 255) return "number of queries must be in [1, 255]";
     if (o.grind > 32) return "grinding factor cannot be greater than 32";
@@ -1038,6 +1038,14 @@ int xfg_prove_burn_mint(xfg_ctx* c, const xfg_burn_inputs* in, uint64_t trace_le
     if (r) return r;
     *out_len = lens[0];
     return st;
+}
+
+int xfg_selftest_field(uint64_t a, uint64_t b, uint64_t* out3) {
+    if (!out3 || a >= P || b >= P) return XFG_INVALID_ARGUMENT;
+    out3[0] = gl_mul(a, b);
+    out3[1] = gl_add(a, b);
+    out3[2] = gl_sub(a, b);
+    return XFG_OK;
 }
 
 int xfg_set_timing(xfg_ctx* c, int enabled) {
