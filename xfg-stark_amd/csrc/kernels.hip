@@ -181,56 +181,28 @@ void launch_trace_gen(const AirConst* air, u64* trace, int logn, int npoly, hipS
     XFG_CHECK_LAUNCH();
 }
 
-// Block-wide batch inversion (Montgomery trick), one value per thread, 256 threads.
-__device__ u64 block_batch_inverse(u64 v, u64* sh /* 2*256 */) {
-    const int tid = threadIdx.x, T = blockDim.x;
-    u64* pre = sh;
-    u64* suf = sh + 256;
-    pre[tid] = v;
-    suf[tid] = v;
-    __syncthreads();
-    // inclusive prefix / suffix products (Hillis-Steele)
-    for (int off = 1; off < T; off <<= 1) {
-        u64 a = pre[tid], b = suf[tid];
-        if (tid >= off) a = gl_mul(a, pre[tid - off]);
-        if (tid + off < T) b = gl_mul(b, suf[tid + off]);
-        __syncthreads();
-        pre[tid] = a;
-        suf[tid] = b;
-        __syncthreads();
-    }
-    u64 total = pre[T - 1];
-    __shared__ u64 inv_total;
-    if (tid == 0) inv_total = gl_inv(total);
-    __syncthreads();
-    u64 r = inv_total;
-    if (tid > 0) r = gl_mul(r, pre[tid - 1]);
-    if (tid + 1 < T) r = gl_mul(r, suf[tid + 1]);
-    __syncthreads();
-    return r;
-}
-
 struct CeArgs {
     const u64* lde;
     const AirConst* air;
     const u64* coeffs;
+    const u64* div;  // [3][2][n]: (x - g^(n-1))/(x^n - 1), 1/(x - 1), 1/(x - g^(n-1)) by (parity, m)
     u64* ce;
     int logn, logbeta;
-    u64 g_last;          // g^(n-1)
-    u64 inv_xn1[2];      // 1/(x^n - 1) for even / odd CE index (x^n = +-7^n)
-    Tables T;
 };
+// One thread per constraint-evaluation point i = 2m + par of the CE domain 7*<w_2n>
+// (ce_to_lde_blowup = beta/2: CE point i is LDE row i*beta/2, i.e. coset t = par*beta/2, row m).
+// Threads walk m fastest inside one parity so the coset-major LDE reads are coalesced.
+// The divisor inverses are data independent and come from a per-(n, beta) table.
 __global__ __launch_bounds__(256) void constraint_eval_kernel(CeArgs a) {
-    __shared__ u64 sh[512];
     const u64 n = 1ULL << a.logn, nce = 2 * n;
     const int proof = blockIdx.y;
-    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;  // grid covers nce exactly
+    const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;  // grid covers nce exactly
+    const u64 par = g >> a.logn, m = g & (n - 1), i = 2 * m + par;
     const AirConst& A = a.air[proof];
     const u64* co = a.coeffs + (u64)proof * 15;
     const u64 beta = 1ULL << a.logbeta;
     const u64* lde = a.lde + (u64)proof * 7 * beta * n;
-    // CE step i <-> LDE index i*beta/2 (ce_to_lde_blowup), coset-major (t, m)
-    const u64 t = (i & 1) ? beta / 2 : 0, m = i >> 1, mn = (m + 1) & (n - 1);
+    const u64 t = par * (beta / 2), mn = (m + 1) & (n - 1);
     u64 cur[7];
 #pragma unroll
     for (int c = 0; c < 7; c++) cur[c] = lde[(((u64)c << a.logbeta) + t) * n + m];
@@ -258,26 +230,17 @@ __global__ __launch_bounds__(256) void constraint_eval_kernel(CeArgs a) {
 #pragma unroll
     for (int c = 0; c < 7; c++) b0 = gl_add(b0, gl_mul(co[7 + c], gl_sub(cur[c], v0[c])));
     u64 b1 = gl_mul(co[14], gl_sub(cur[4], 3));
-    // x = 7 w_2n^i ; divisors (x - 1), (x - g^(n-1)), (x^n - 1)
-    const u64 x = gl_mul(GEN, tw_pow(a.T, a.logn + 1, i));
-    const u64 xa = gl_sub(x, 1), xb = gl_sub(x, a.g_last);
-    u64 inv_ab = block_batch_inverse(gl_mul(xa, xb), sh);
-    u64 inv_a = gl_mul(inv_ab, xb), inv_b = gl_mul(inv_ab, xa);
-    u64 val = gl_mul(gl_mul(tr, xb), a.inv_xn1[i & 1]);
-    val = gl_add(val, gl_mul(b0, inv_a));
-    val = gl_add(val, gl_mul(b1, inv_b));
+    const u64 di = par * n + m;
+    u64 val = gl_mul(tr, a.div[di]);
+    val = gl_add(val, gl_mul(b0, a.div[nce + di]));
+    val = gl_add(val, gl_mul(b1, a.div[2 * nce + di]));
     a.ce[(u64)proof * nce + i] = val;
 }
-void launch_constraint_eval(const u64* lde, const AirConst* air, const u64* coeffs, u64* ce, int logn, int logbeta,
-                            const Tables& T, int npoly, hipStream_t s) {
+void launch_constraint_eval(const u64* lde, const AirConst* air, const u64* coeffs, const u64* div, u64* ce, int logn,
+                            int logbeta, int npoly, hipStream_t s) {
     CeArgs a;
-    a.lde = lde; a.air = air; a.coeffs = coeffs; a.ce = ce; a.logn = logn; a.logbeta = logbeta; a.T = T;
-    u64 n = 1ULL << logn;
-    a.g_last = gl_pow(gl_root(logn), n - 1);
-    u64 sn = gl_pow(GEN, n);
-    a.inv_xn1[0] = gl_inv(gl_sub(sn, 1));
-    a.inv_xn1[1] = gl_inv(gl_sub(gl_neg(sn), 1));
-    u64 nce = 2 * n;
+    a.lde = lde; a.air = air; a.coeffs = coeffs; a.div = div; a.ce = ce; a.logn = logn; a.logbeta = logbeta;
+    u64 nce = 2ULL << logn;
     int threads = nce < 256 ? (int)nce : 256;
     dim3 g((unsigned)(nce / threads), npoly);
     hipLaunchKernelGGL(constraint_eval_kernel, g, dim3(threads), 0, s, a);

@@ -54,8 +54,9 @@ void launch_tree_top(Digest* nodes, u64 node_stride, u64 count, int npoly, hipSt
 // ---- AIR ----
 void launch_trace_gen(const AirConst* air, u64* trace, int logn, int npoly, hipStream_t s);
 // composition evaluations over the CE domain 7*<w_2n> (natural order) from the trace LDE
-void launch_constraint_eval(const u64* lde, const AirConst* air, const u64* coeffs /*[B][15]*/, u64* ce, int logn,
-                            int logbeta, const Tables& T, int npoly, hipStream_t s);
+// div = constraint divisor table [3][2][n] from ce_divisor_table()
+void launch_constraint_eval(const u64* lde, const AirConst* air, const u64* coeffs /*[B][15]*/, const u64* div,
+                            u64* ce, int logn, int logbeta, int npoly, hipStream_t s);
 
 // ---- OOD / DEEP ----
 void launch_ood(const u64* coef, const u64* hcoef, const u64* zpts /*[B][2]*/, u64* partial, u64* ood /*[B][15]*/,

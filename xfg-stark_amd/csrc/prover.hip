@@ -309,7 +309,38 @@ struct HBuf {
 struct TablesHost {
     int LM = -1;
     DBuf<u64> tw, pow7, ipow7;
+    int ce_logn = -1;
+    DBuf<u64> ce_div;  // constraint divisor table for trace length 2^ce_logn
 };
+
+// Data-independent constraint divisors on the CE domain x_i = 7 w_2n^i (i = 2m + par), laid out
+// [3][par][m]: transition (x - g^(n-1)) / (x^n - 1), boundary 1/(x - 1) and 1/(x - g^(n-1))
+// (ConstraintDivisor::from_transition / from_assertion). Batch-inverted once per trace length.
+static std::vector<u64> ce_divisor_table(int logn) {
+    const u64 n = 1ULL << logn, nce = 2 * n;
+    const u64 w = gl_root(logn + 1), g_last = gl_pow(gl_root(logn), n - 1);
+    const u64 sn = gl_pow(GEN, n);
+    const u64 inv_xn1[2] = {gl_inv(gl_sub(sn, 1)), gl_inv(gl_sub(gl_neg(sn), 1))};
+    std::vector<u64> xa(nce), xb(nce), prod(nce);
+    u64 x = GEN, acc = 1;
+    for (u64 i = 0; i < nce; i++, x = gl_mul(x, w)) {
+        xa[i] = gl_sub(x, 1);
+        xb[i] = gl_sub(x, g_last);
+        acc = gl_mul(acc, gl_mul(xa[i], xb[i]));
+        prod[i] = acc;
+    }
+    u64 inv = gl_inv(acc);
+    std::vector<u64> out(3 * nce);
+    for (u64 i = nce; i-- > 0;) {
+        u64 inv_ab = i ? gl_mul(inv, prod[i - 1]) : inv;  // 1 / (xa_i xb_i)
+        inv = gl_mul(inv, gl_mul(xa[i], xb[i]));
+        const u64 par = i & 1, m = i >> 1, di = par * n + m;
+        out[di] = gl_mul(xb[i], inv_xn1[par]);
+        out[nce + di] = gl_mul(inv_ab, xb[i]);
+        out[2 * nce + di] = gl_mul(inv_ab, xa[i]);
+    }
+    return out;
+}
 
 static const char* STAGE_NAMES[] = {"trace_lde",     "trace_commit", "constraint_eval", "composition",
                                     "comp_commit",   "ood",          "deep",            "fri",
@@ -387,6 +418,15 @@ static void ensure_tables(xfg_ctx* c, int LM) {
     HIPCHK(hipMemcpy(c->tables.ipow7.p, ip7.data(), M * 8, hipMemcpyHostToDevice));
     c->tables.LM = LM;
 }
+static const u64* ensure_ce_table(xfg_ctx* c, int logn) {
+    if (c->tables.ce_logn != logn) {
+        std::vector<u64> t = ce_divisor_table(logn);
+        c->tables.ce_div.ensure(t.size());
+        HIPCHK(hipMemcpy(c->tables.ce_div.p, t.data(), t.size() * 8, hipMemcpyHostToDevice));
+        c->tables.ce_logn = logn;
+    }
+    return c->tables.ce_div.p;
+}
 static Tables tables_of(xfg_ctx* c) {
     Tables T;
     T.tw = c->tables.tw.p;
@@ -419,8 +459,8 @@ static void stage_mark(Lane* c, int k) {
 }
 
 // the batched prover: jobs[i].air filled; trace_host optional ([B][7][n], else generated on device)
-static void prove_lane(Lane* c, const Tables& T, ProofJob* jobs_p, int B, const u64* trace_host, u64 n,
-                       const Opts& o) {
+static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jobs_p, int B, const u64* trace_host,
+                       u64 n, const Opts& o) {
     auto t_host0 = std::chrono::steady_clock::now();
     struct JobSpan {
         ProofJob* p;
@@ -509,7 +549,7 @@ static void prove_lane(Lane* c, const Tables& T, ProofJob* jobs_p, int B, const 
     HIPCHK(hipMemcpyAsync(c->coeffs.p, co, (size_t)B * 15 * 8, hipMemcpyHostToDevice, s));
 
     // ---- 3. constraint evaluation + composition polynomial + commitment
-    launch_constraint_eval(c->lde.p, c->air.p, c->coeffs.p, c->ce.p, logn, logbeta, T, B, s);
+    launch_constraint_eval(c->lde.p, c->air.p, c->coeffs.p, ce_div, c->ce.p, logn, logbeta, B, s);
     stage_mark(c, 3);
     launch_interpolate(c->ce.p, 2 * n, c->hcoef.p, n, c->scratch.p, B, logn + 1, true, n, T, s);
     launch_lde(c->hcoef.p, n, c->hlde.p, c->scratch.p, B, logn, logbeta, T, s);
@@ -811,12 +851,13 @@ static void prove_jobs(xfg_ctx* c, std::vector<ProofJob>& jobs, const u64* trace
     const int B = (int)jobs.size();
     ensure_tables(c, (int)(ilog2(n) + ilog2(o.beta)));
     const Tables T = tables_of(c);
+    const u64* ce_div = ensure_ce_table(c, (int)ilog2(n));
     int nl = std::max(1, std::min(MAX_LANES, B / MIN_PER_LANE));
     if (trace_host) nl = 1;
     ensure_lanes(c, nl);
     for (auto& L : c->lanes) L->timing = c->timing;
     if (nl == 1) {
-        prove_lane(c->lanes[0].get(), T, jobs.data(), B, trace_host, n, o);
+        prove_lane(c->lanes[0].get(), T, ce_div, jobs.data(), B, trace_host, n, o);
         return;
     }
     std::vector<std::thread> th;
@@ -828,7 +869,7 @@ static void prove_jobs(xfg_ctx* c, std::vector<ProofJob>& jobs, const u64* trace
         th.emplace_back([&, l, b0, b1] {
             try {
                 HIPCHK(hipSetDevice(c->device));
-                prove_lane(c->lanes[l].get(), T, jobs.data() + b0, b1 - b0, nullptr, n, o);
+                prove_lane(c->lanes[l].get(), T, ce_div, jobs.data() + b0, b1 - b0, nullptr, n, o);
             } catch (...) {
                 errs[l] = std::current_exception();
             }
@@ -899,6 +940,7 @@ void xfg_ctx_destroy(xfg_ctx* c) {
     c->tables.tw.release();
     c->tables.pow7.release();
     c->tables.ipow7.release();
+    c->tables.ce_div.release();
     delete c;
 }
 
