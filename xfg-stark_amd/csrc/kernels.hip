@@ -29,41 +29,29 @@ __device__ __forceinline__ u64 tw_ipow(const Tables& T, int k, u64 e) {
 }
 
 // ============================================================================ Merkle
-// builds `levels` levels above the per-thread nodes held in lds[0..nthreads) and writes them;
-// node index of thread i at the base level is base_idx + i
-__device__ __forceinline__ void lds_subtree(Digest* lds, Digest mine, Digest* nodes, u64 base_idx, int levels) {
-    const int tid = threadIdx.x;
-    lds[tid] = mine;
-    __syncthreads();
-    for (int l = 1; l <= levels; l++) {
-        int cnt = blockDim.x >> l;
-        Digest d;
-        if (tid < cnt) d = b3_merge(lds[2 * tid], lds[2 * tid + 1]);
-        __syncthreads();
-        if (tid < cnt) {
-            lds[tid] = d;
-            nodes[(base_idx >> l) + tid] = d;
-        }
-        __syncthreads();
-    }
-}
+// Heap layout per tree: nodes[1] = root, nodes[i] = H(nodes[2i] || nodes[2i+1]), leaf k at L + k
+// (MerkleTree::new / build_merkle_nodes, winter-crypto 0.8.3). For the LDE commitments only the
+// levels >= log2(beta) are stored (heap [1, 2n)): the 2^log2(beta) leaves of LDE row m (one per
+// coset, coset-major layout) form a register-resident subtree whose top is heap node n + m. The
+// few leaves / low nodes a proof opens are recomputed from the LDE by open_rows_kernel.
 
-// subtree over leaves t = T0 .. T0 + 2^LOG - 1 of LDE row m (leaf k = (m << LOGB) + t); compile-time
-// recursion keeps every intermediate digest in registers
+// subtree over the leaves t = T0 .. T0 + 2^LOG - 1 of LDE row m; compile-time recursion keeps
+// every intermediate digest in registers. If `local` is non-null the nodes are also written to
+// a local heap (slot 1 = top, leaves at 2^LOGB + t).
 template <int NC, int LOGB, int LOG, int T0>
-__device__ __forceinline__ Digest lde_subtree(const u64* base, u64 n, u64 m, Digest* nodes, u64 L) {
+__device__ __forceinline__ Digest lde_subtree(const u64* base, u64 n, u64 m, Digest* local) {
     if constexpr (LOG == 0) {
         u64 row[NC];
 #pragma unroll
         for (int c = 0; c < NC; c++) row[c] = base[((u64)c * (1 << LOGB) + T0) * n + m];
         Digest d = b3_hash_elems<NC>(row);
-        nodes[L + (m << LOGB) + T0] = d;
+        if (local) local[(1 << LOGB) + T0] = d;
         return d;
     } else {
-        Digest l = lde_subtree<NC, LOGB, LOG - 1, T0>(base, n, m, nodes, L);
-        Digest r = lde_subtree<NC, LOGB, LOG - 1, T0 + (1 << (LOG - 1))>(base, n, m, nodes, L);
+        Digest l = lde_subtree<NC, LOGB, LOG - 1, T0>(base, n, m, local);
+        Digest r = lde_subtree<NC, LOGB, LOG - 1, T0 + (1 << (LOG - 1))>(base, n, m, local);
         Digest p = b3_merge(l, r);
-        nodes[(L + (m << LOGB) + T0) >> LOG] = p;
+        if (local) local[((1 << LOGB) + T0) >> LOG] = p;
         return p;
     }
 }
@@ -71,57 +59,114 @@ __device__ __forceinline__ Digest lde_subtree(const u64* base, u64 n, u64 m, Dig
 template <int NC, int LOGB>
 __global__ __launch_bounds__(256) void leaves_lde_kernel(const u64* lde, Digest* nodes_all, u64 node_stride,
                                                          int logn) {
-    __shared__ Digest lds[256];
-    constexpr int B = 1 << LOGB;
-    const u64 n = 1ULL << logn, L = n << LOGB;
+    const u64 n = 1ULL << logn;
     const int proof = blockIdx.y;
-    const u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x;  // grid covers n exactly
-    const u64* base = lde + (u64)proof * NC * B * n;
-    Digest* nodes = nodes_all + (u64)proof * node_stride;
-    Digest top = lde_subtree<NC, LOGB, LOGB, 0>(base, n, m, nodes, L);
-    int levels = 31 - __clz(blockDim.x);
-    lds_subtree(lds, top, nodes, n + (u64)blockIdx.x * blockDim.x, levels);
+    const u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= n) return;
+    const u64* base = lde + (u64)proof * NC * (1 << LOGB) * n;
+    nodes_all[(u64)proof * node_stride + n + m] = lde_subtree<NC, LOGB, LOGB, 0>(base, n, m, nullptr);
 }
 
-template <int NC>
-static void leaves_lde_dispatch(int logbeta, dim3 g, dim3 b, hipStream_t s, const u64* lde, Digest* nodes,
-                                u64 stride, int logn) {
-    switch (logbeta) {
-        case 1: hipLaunchKernelGGL((leaves_lde_kernel<NC, 1>), g, b, 0, s, lde, nodes, stride, logn); break;
-        case 2: hipLaunchKernelGGL((leaves_lde_kernel<NC, 2>), g, b, 0, s, lde, nodes, stride, logn); break;
-        case 3: hipLaunchKernelGGL((leaves_lde_kernel<NC, 3>), g, b, 0, s, lde, nodes, stride, logn); break;
-        case 4: hipLaunchKernelGGL((leaves_lde_kernel<NC, 4>), g, b, 0, s, lde, nodes, stride, logn); break;
-        default: break;
-    }
+// openings: recompute the local subtree heaps of selected rows; entry e = proof << logn | m
+template <int NC, int LOGB>
+__global__ __launch_bounds__(64) void open_rows_kernel(const u64* lde, const u64* entries, u64 count, Digest* out,
+                                                       int logn) {
+    const u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= count) return;
+    const u64 n = 1ULL << logn, ent = entries[e];
+    const u64 proof = ent >> logn, m = ent & (n - 1);
+    const u64* base = lde + proof * NC * (1 << LOGB) * n;
+    lde_subtree<NC, LOGB, LOGB, 0>(base, n, m, out + e * (2 << LOGB));
 }
+
+#define XFG_LOGB_DISPATCH(KERNEL, NC, logbeta, ...)                                            \
+    switch (logbeta) {                                                                          \
+        case 1: hipLaunchKernelGGL((KERNEL<NC, 1>), __VA_ARGS__); break;                        \
+        case 2: hipLaunchKernelGGL((KERNEL<NC, 2>), __VA_ARGS__); break;                        \
+        case 3: hipLaunchKernelGGL((KERNEL<NC, 3>), __VA_ARGS__); break;                        \
+        case 4: hipLaunchKernelGGL((KERNEL<NC, 4>), __VA_ARGS__); break;                        \
+        default: break;                                                                         \
+    }
+
 void launch_leaves_lde(const u64* lde, int nc, Digest* nodes, u64 node_stride, int npoly, int logn, int logbeta,
                        hipStream_t s) {
     u64 n = 1ULL << logn;
-    int threads = n < 256 ? (int)n : 256;
-    dim3 g((unsigned)(n / threads), npoly), b(threads);
-    if (nc == 7) leaves_lde_dispatch<7>(logbeta, g, b, s, lde, nodes, node_stride, logn);
-    else leaves_lde_dispatch<1>(logbeta, g, b, s, lde, nodes, node_stride, logn);
+    dim3 g((unsigned)((n + 255) / 256), npoly), b(256);
+    if (nc == 7) { XFG_LOGB_DISPATCH(leaves_lde_kernel, 7, logbeta, g, b, 0, s, lde, nodes, node_stride, logn) }
+    else { XFG_LOGB_DISPATCH(leaves_lde_kernel, 1, logbeta, g, b, 0, s, lde, nodes, node_stride, logn) }
+    XFG_CHECK_LAUNCH();
+}
+void launch_open_rows(const u64* lde, int nc, const u64* entries, u64 count, Digest* out, int logn, int logbeta,
+                      hipStream_t s) {
+    if (!count) return;
+    dim3 g((unsigned)((count + 63) / 64)), b(64);
+    if (nc == 7) { XFG_LOGB_DISPATCH(open_rows_kernel, 7, logbeta, g, b, 0, s, lde, entries, count, out, logn) }
+    else { XFG_LOGB_DISPATCH(open_rows_kernel, 1, logbeta, g, b, 0, s, lde, entries, count, out, logn) }
     XFG_CHECK_LAUNCH();
 }
 
-__global__ __launch_bounds__(256) void tree_levels_kernel(Digest* nodes_all, u64 node_stride, u64 count, int levels) {
-    __shared__ Digest lds[256];
+// one thread per node of level `count >> H`: merges its 2^H descendants at level `count`
+// (heap [count, 2 count)) in registers and writes the H levels above them
+template <int H>
+__device__ __forceinline__ Digest up_subtree(const Digest* src, Digest* nodes, u64 first, int lvl_from_top) {
+    (void)lvl_from_top;
+    if constexpr (H == 0) {
+        return src[0];
+    } else {
+        Digest l = up_subtree<H - 1>(src, nodes, first, 0);
+        Digest r = up_subtree<H - 1>(src + (1 << (H - 1)), nodes, first + (1ULL << (H - 1)), 0);
+        Digest p = b3_merge(l, r);
+        nodes[first >> H] = p;
+        return p;
+    }
+}
+template <int H>
+__global__ __launch_bounds__(256) void tree_up_kernel(Digest* nodes_all, u64 node_stride, u64 count) {
+    const u64 idx = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (count >> H)) return;
     Digest* nodes = nodes_all + (u64)blockIdx.y * node_stride;
-    const u64 first = count + (u64)blockIdx.x * (2 * blockDim.x);
+    const u64 first = count + (idx << H);
+    Digest ch[1 << H];
+#pragma unroll
+    for (int k = 0; k < (1 << H); k++) ch[k] = nodes[first + k];
+    up_subtree<H>(ch, nodes, first, 0);
+}
+// last levels (count <= 512): one block per tree, LDS
+__global__ __launch_bounds__(256) void tree_top_kernel(Digest* nodes_all, u64 node_stride, u64 count) {
+    __shared__ Digest lds[256];
+    Digest* nodes = nodes_all + (u64)blockIdx.x * node_stride;
     const int tid = threadIdx.x;
-    Digest d = b3_merge(nodes[first + 2 * tid], nodes[first + 2 * tid + 1]);
-    nodes[(first >> 1) + tid] = d;
-    lds_subtree(lds, d, nodes, first >> 1, levels - 1);
+    for (u64 c = count; c > 1; c >>= 1) {
+        const u64 half = c >> 1;
+        Digest d;
+        if (tid < (int)half) {
+            if (c == count) d = b3_merge(nodes[c + 2 * tid], nodes[c + 2 * tid + 1]);
+            else d = b3_merge(lds[2 * tid], lds[2 * tid + 1]);
+        }
+        __syncthreads();
+        if (tid < (int)half) {
+            lds[tid] = d;
+            nodes[half + tid] = d;
+        }
+        __syncthreads();
+    }
 }
 void launch_tree_top(Digest* nodes, u64 node_stride, u64 count, int npoly, hipStream_t s) {
-    while (count > 1) {
+    while (count > 512) {
         int lg = 0;
         while ((1ULL << (lg + 1)) <= count) lg++;
-        int levels = lg < 9 ? lg : 9;
-        int threads = 1 << (levels - 1);
-        dim3 g((unsigned)(count >> levels), npoly);
-        hipLaunchKernelGGL(tree_levels_kernel, g, dim3(threads), 0, s, nodes, node_stride, count, levels);
-        count >>= levels;
+        int h = lg - 9 < 3 ? lg - 9 : 3;
+        u64 outc = count >> h;
+        dim3 g((unsigned)((outc + 255) / 256), npoly);
+        if (h == 3) hipLaunchKernelGGL(tree_up_kernel<3>, g, dim3(256), 0, s, nodes, node_stride, count);
+        else if (h == 2) hipLaunchKernelGGL(tree_up_kernel<2>, g, dim3(256), 0, s, nodes, node_stride, count);
+        else hipLaunchKernelGGL(tree_up_kernel<1>, g, dim3(256), 0, s, nodes, node_stride, count);
+        count = outc;
+    }
+    if (count > 1) {
+        int threads = (int)(count / 2);
+        threads = threads < 64 ? 64 : threads;
+        hipLaunchKernelGGL(tree_top_kernel, dim3(npoly), dim3(threads), 0, s, nodes, node_stride, count);
     }
     XFG_CHECK_LAUNCH();
 }
@@ -133,27 +178,24 @@ __device__ __forceinline__ u64 layer_at(const u64* base, bool coset_major, int l
     return base[(t << logn) + m];
 }
 
+// FRI layer leaves (hash_values::<H, E, 8> over transpose_slice rows): leaf i = H(values at
+// natural indices i + k*rows, k < 8). All leaves are stored (layers are N/8 and smaller).
 __global__ __launch_bounds__(256) void fri_leaves_kernel(const u64* vals, u64 val_stride, int coset_major, int logn,
                                                          int logbeta, u64 rows, Digest* nodes_all, u64 node_stride) {
-    __shared__ Digest lds[256];
     const int proof = blockIdx.y;
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= rows) return;
     const u64* base = vals + (u64)proof * val_stride;
-    Digest* nodes = nodes_all + (u64)proof * node_stride;
     u64 v[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) v[k] = layer_at(base, coset_major, logn, logbeta, i + (u64)k * rows);
-    Digest d = b3_hash_elems<8>(v);
-    nodes[rows + i] = d;
-    int levels = 31 - __clz(blockDim.x);
-    lds_subtree(lds, d, nodes, rows + (u64)blockIdx.x * blockDim.x, levels);
+    nodes_all[(u64)proof * node_stride + rows + i] = b3_hash_elems<8>(v);
 }
 void launch_fri_leaves(const u64* vals, u64 val_stride, bool coset_major, int logn, int logbeta, u64 rows,
                        Digest* nodes, u64 node_stride, int npoly, hipStream_t s) {
-    int threads = rows < 256 ? (int)rows : 256;
-    dim3 g((unsigned)(rows / threads), npoly);
-    hipLaunchKernelGGL(fri_leaves_kernel, g, dim3(threads), 0, s, vals, val_stride, coset_major ? 1 : 0, logn,
-                       logbeta, rows, nodes, node_stride);
+    dim3 g((unsigned)((rows + 255) / 256), npoly);
+    hipLaunchKernelGGL(fri_leaves_kernel, g, dim3(256), 0, s, vals, val_stride, coset_major ? 1 : 0, logn, logbeta,
+                       rows, nodes, node_stride);
     XFG_CHECK_LAUNCH();
 }
 

@@ -41,11 +41,15 @@ void launch_interpolate(const u64* evals, u64 in_stride, u64* out, u64 out_strid
                         bool off7, u64 keep, const Tables& T, hipStream_t s);
 
 // ---- Merkle (heap layout: nodes[1] = root, nodes[L + i] = leaf i) ----
-// leaves = rows of an NC-column coset-major LDE (NC in {1, 7}); builds the in-block subtree levels
+// LDE commitments store levels >= log2(beta) only: node_stride >= 2n, top of row m at n + m
 void launch_leaves_lde(const u64* lde, int nc, Digest* nodes, u64 node_stride, int npoly, int logn, int logbeta,
                        hipStream_t s);
+// recompute the local subtree heap (2 * beta digests, slot 1 = top, leaf t at beta + t) of LDE
+// rows entries[e] = proof << logn | m, for Merkle openings
+void launch_open_rows(const u64* lde, int nc, const u64* entries, u64 count, Digest* out, int logn, int logbeta,
+                      hipStream_t s);
 // FRI layer leaves: row i = values at natural indices i + k*rows, k < 8 (coset-major source when
-// coset_major, else natural); also writes in-block subtree levels
+// coset_major, else natural); all leaves stored at nodes[rows + i]
 void launch_fri_leaves(const u64* vals, u64 val_stride, bool coset_major, int logn, int logbeta, u64 rows,
                        Digest* nodes, u64 node_stride, int npoly, hipStream_t s);
 // completes the tree above level `count` (nodes [count, 2count) present) up to the root

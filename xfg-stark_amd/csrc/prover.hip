@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <map>
@@ -481,11 +482,11 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     c->coef.ensure((size_t)B * 7 * n);
     c->scratch.ensure((size_t)B * 7 * N);
     c->lde.ensure((size_t)B * 7 * N);
-    c->tnodes.ensure((size_t)B * 2 * N);
+    c->tnodes.ensure((size_t)B * 2 * n);
     c->ce.ensure((size_t)B * 2 * n);
     c->hcoef.ensure((size_t)B * n);
     c->hlde.ensure((size_t)B * N);
-    c->hnodes.ensure((size_t)B * 2 * N);
+    c->hnodes.ensure((size_t)B * 2 * n);
     c->zpts.ensure((size_t)B * 2);
     c->partial.ensure((size_t)B * 15 * (n / 8 / 256 + 2));
     c->ood.ensure((size_t)B * 15);
@@ -529,11 +530,11 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     launch_interpolate(c->trace.p, n, c->coef.p, n, c->scratch.p, B * 7, logn, false, n, T, s);
     launch_lde(c->coef.p, n, c->lde.p, c->scratch.p, B * 7, logn, logbeta, T, s);
     stage_mark(c, 1);
-    launch_leaves_lde(c->lde.p, 7, c->tnodes.p, 2 * N, B, logn, logbeta, s);
-    launch_tree_top(c->tnodes.p, 2 * N, n / std::min<u64>(n, 256), B, s);
+    launch_leaves_lde(c->lde.p, 7, c->tnodes.p, 2 * n, B, logn, logbeta, s);
+    launch_tree_top(c->tnodes.p, 2 * n, n, B, s);
     Digest* roots = c->h_roots.ensure(B);
     stage_mark(c, 2);
-    fetch_roots(c, c->tnodes.p, 2 * N, B, roots);
+    fetch_roots(c, c->tnodes.p, 2 * n, B, roots);
 
     // ---- 2. constraint composition coefficients (7 transition + 8 boundary)
     u64* co = c->h_co.ensure((size_t)B * 15);
@@ -554,10 +555,10 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     launch_interpolate(c->ce.p, 2 * n, c->hcoef.p, n, c->scratch.p, B, logn + 1, true, n, T, s);
     launch_lde(c->hcoef.p, n, c->hlde.p, c->scratch.p, B, logn, logbeta, T, s);
     stage_mark(c, 4);
-    launch_leaves_lde(c->hlde.p, 1, c->hnodes.p, 2 * N, B, logn, logbeta, s);
-    launch_tree_top(c->hnodes.p, 2 * N, n / std::min<u64>(n, 256), B, s);
+    launch_leaves_lde(c->hlde.p, 1, c->hnodes.p, 2 * n, B, logn, logbeta, s);
+    launch_tree_top(c->hnodes.p, 2 * n, n, B, s);
     stage_mark(c, 5);
-    fetch_roots(c, c->hnodes.p, 2 * N, B, roots);
+    fetch_roots(c, c->hnodes.p, 2 * n, B, roots);
 
     // ---- 4. OOD point and frame
     const u64 g = gl_root(logn);
@@ -621,7 +622,7 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         const u64* src = cm ? c->f0.p : c->flayer[l].p;
         const u64 sstride = cm ? N : D[l];
         launch_fri_leaves(src, sstride, cm, logn, logbeta, rows, c->fnodes[l].p, 2 * rows, B, s);
-        launch_tree_top(c->fnodes[l].p, 2 * rows, rows / std::min<u64>(rows, 256), B, s);
+        launch_tree_top(c->fnodes[l].p, 2 * rows, rows, B, s);
         fetch_roots(c, c->fnodes[l].p, 2 * rows, B, roots);
         for (int b = 0; b < B; b++) {
             auto& j = jobs[b];
@@ -653,12 +654,15 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     HIPCHK(hipStreamSynchronize(s));
 
     // ---- 7. grinding + query positions, gather lists
-    std::vector<u64> vidx_lde, vidx_h, vidx_f0;
-    std::vector<std::vector<u64>> vidx_f(nl + 1);
-    std::vector<u64> didx_t, didx_h;
-    std::vector<std::vector<u64>> didx_f(nl + 1);
+    // LDE trees store heap levels >= log2(beta) (indices < 2n); lower nodes of an opened row are
+    // recomputed by launch_open_rows (local heap: 2 * beta slots per row)
+    const u64 stored_lim = 2 * n, LB = beta;
+    std::vector<u64> vidx_lde, vidx_h, didx_t, didx_h, open_ent;
+    std::vector<std::vector<u64>> vidx_f(nl + 1), didx_f(nl + 1);
     struct Layout {
-        std::vector<BatchOpening> ops;  // trace, comp, fri layers
+        BatchOpening op;                     // trace / constraint trees (same positions)
+        std::vector<int64_t> ref;            // per node: >= 0 stored ordinal, < 0 -(open slot + 1)
+        std::vector<BatchOpening> fops;      // FRI layers
         std::vector<std::vector<u64>> fpos;
     };
     std::vector<Layout> lay(B);
@@ -690,10 +694,28 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
             for (int col = 0; col < 7; col++) vidx_lde.push_back((((u64)b * 7 + col) * beta + t) * n + m);
             vidx_h.push_back(((u64)b * beta + t) * n + m);
         }
-        L.ops.push_back(plan_batch_opening(pos, N));
-        L.ops.push_back(plan_batch_opening(pos, N));
-        for (auto& v : L.ops[0].vecs) for (u64 x : v) didx_t.push_back((u64)b * 2 * N + x);
-        for (auto& v : L.ops[1].vecs) for (u64 x : v) didx_h.push_back((u64)b * 2 * N + x);
+        // rows whose subtrees are recomputed: positions are sorted, so rows come sorted
+        std::vector<u64> rows_b;
+        for (u64 k : pos)
+            if (rows_b.empty() || rows_b.back() != (k >> logbeta)) rows_b.push_back(k >> logbeta);
+        const u64 ent0 = open_ent.size();
+        for (u64 m : rows_b) open_ent.push_back(((u64)b << logn) | m);
+        L.op = plan_batch_opening(pos, N);
+        int64_t stored_ord = 0;
+        for (auto& v : L.op.vecs)
+            for (u64 h : v) {
+                if (h < stored_lim) {
+                    didx_t.push_back((u64)b * stored_lim + h);
+                    didx_h.push_back((u64)b * stored_lim + h);
+                    L.ref.push_back(stored_ord++);
+                } else {
+                    unsigned lvl = (unsigned)(logn + logbeta) - (63 - __builtin_clzll(h));  // 0 = leaves
+                    u64 off = h - (N >> lvl), span = logbeta - lvl;
+                    u64 m = off >> span, local = (1ULL << span) + (off & ((1ULL << span) - 1));
+                    u64 e = ent0 + (std::lower_bound(rows_b.begin(), rows_b.end(), m) - rows_b.begin());
+                    L.ref.push_back(-(int64_t)(e * 2 * LB + local) - 1);
+                }
+            }
         std::vector<u64> fp = pos;
         for (unsigned l = 0; l < nl; l++) {
             u64 rows = D[l] / 8;
@@ -705,8 +727,8 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
                     if (l == 0) vidx_f[0].push_back(((u64)b * beta + (K & (beta - 1))) * n + (K >> logbeta));
                     else vidx_f[l].push_back((u64)b * D[l] + K);
                 }
-            L.ops.push_back(plan_batch_opening(fp, rows));
-            for (auto& v : L.ops.back().vecs) for (u64 x : v) didx_f[l].push_back((u64)b * 2 * rows + x);
+            L.fops.push_back(plan_batch_opening(fp, rows));
+            for (auto& v : L.fops.back().vecs) for (u64 x : v) didx_f[l].push_back((u64)b * 2 * rows + x);
         }
     }
     // one index buffer, one value buffer, one digest buffer; segment per source
@@ -724,9 +746,11 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     add_seg(didx_h, dseg);
     for (unsigned l = 0; l < nl; l++) add_seg(didx_f[l], dseg);
     size_t ndig = allidx.size() - nvals;
+    const size_t nent = open_ent.size(), nopen = nent * 2 * LB;
+    allidx.insert(allidx.end(), open_ent.begin(), open_ent.end());
     c->gidx.ensure(allidx.size());
     c->gval.ensure(nvals);
-    c->gdig.ensure(ndig);
+    c->gdig.ensure(ndig + 2 * nopen);
     u64* hidx = c->h_idx.ensure(allidx.size());
     memcpy(hidx, allidx.data(), allidx.size() * 8);
     HIPCHK(hipMemcpyAsync(c->gidx.p, hidx, allidx.size() * 8, hipMemcpyHostToDevice, s));
@@ -744,15 +768,21 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
             launch_gather_digest(src, c->gidx.p + dseg[k].first, c->gdig.p + dof, dseg[k].second, s);
             dof += dseg[k].second;
         }
+        const u64* ent = c->gidx.p + nvals + ndig;
+        launch_open_rows(c->lde.p, 7, ent, nent, c->gdig.p + ndig, logn, logbeta, s);
+        launch_open_rows(c->hlde.p, 1, ent, nent, c->gdig.p + ndig + nopen, logn, logbeta, s);
     }
     u64* gv = c->h_gv.ensure(nvals);
-    Digest* gd = c->h_gd.ensure(ndig);
+    Digest* gd = c->h_gd.ensure(ndig + 2 * nopen);
     if (nvals) HIPCHK(hipMemcpyAsync(gv, c->gval.p, nvals * 8, hipMemcpyDeviceToHost, s));
-    if (ndig) HIPCHK(hipMemcpyAsync(gd, c->gdig.p, ndig * sizeof(Digest), hipMemcpyDeviceToHost, s));
+    if (ndig + 2 * nopen)
+        HIPCHK(hipMemcpyAsync(gd, c->gdig.p, (ndig + 2 * nopen) * sizeof(Digest), hipMemcpyDeviceToHost, s));
     stage_mark(c, 9);
     HIPCHK(hipStreamSynchronize(s));
 
     // ---- 8. StarkProof::to_bytes (DESIGN.md "Proof format")
+    const Digest* open_t = gd + ndig;
+    const Digest* open_h = gd + ndig + nopen;
     size_t cur_lde = 0, cur_h = vidx_lde.size(), cur_t = 0, cur_hd = didx_t.size();
     std::vector<size_t> cur_fv(nl), cur_fd(nl);
     {
@@ -768,6 +798,20 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
             p.u8(v.size());
             p.put(&gd[cursor], 32 * v.size());
             cursor += v.size();
+        }
+        w.u32(p.b.size());
+        w.put(p.b.data(), p.b.size());
+    };
+    auto write_lde_paths = [&](BW& w, const Layout& L, size_t& cursor, const Digest* open) {
+        BW p;
+        p.u8(L.op.vecs.size());
+        size_t r = 0;
+        for (auto& v : L.op.vecs) {
+            p.u8(v.size());
+            for (size_t k = 0; k < v.size(); k++, r++) {
+                int64_t ref = L.ref[r];
+                p.digest(ref >= 0 ? gd[cursor++] : open[-ref - 1]);
+            }
         }
         w.u32(p.b.size());
         w.put(p.b.data(), p.b.size());
@@ -789,12 +833,12 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         w.u32(nu * 7 * 8);
         w.u64s(&gv[cur_lde], nu * 7);
         cur_lde += nu * 7;
-        write_paths(w, lay[b].ops[0], cur_t);
+        write_lde_paths(w, lay[b], cur_t, open_t);
         // constraint queries
         w.u32(nu * 8);
         w.u64s(&gv[cur_h], nu);
         cur_h += nu;
-        write_paths(w, lay[b].ops[1], cur_hd);
+        write_lde_paths(w, lay[b], cur_hd, open_h);
         // OOD frame
         w.u16(1 + 14 * 8);
         w.u8(2);
@@ -808,7 +852,7 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
             w.u32(nk * 8 * 8);
             w.u64s(&gv[cur_fv[l]], nk * 8);
             cur_fv[l] += nk * 8;
-            write_paths(w, lay[b].ops[2 + l], cur_fd[l]);
+            write_paths(w, lay[b].fops[l], cur_fd[l]);
         }
         w.u16(rem_len * 8);
         for (u64 i = 0; i < rem_len; i++) w.u64_(remh[(size_t)b * rem_len + i]);
@@ -843,15 +887,20 @@ static void ensure_lanes(xfg_ctx* c, size_t k) {
         for (auto& e : c->lanes.back()->ev) HIPCHK(hipEventCreate(&e));
     }
 }
-// proofs per lane below which a batch is not split (each lane runs a full pipeline)
-static const int MIN_PER_LANE = 8;
-static const int MAX_LANES = 2;
+// proofs per lane below which a batch is not split (each lane runs a full pipeline); overridable
+// with XFG_LANES / XFG_MIN_PER_LANE for tuning
+static int env_int(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v && *v ? atoi(v) : dflt;
+}
 
 static void prove_jobs(xfg_ctx* c, std::vector<ProofJob>& jobs, const u64* trace_host, u64 n, const Opts& o) {
     const int B = (int)jobs.size();
     ensure_tables(c, (int)(ilog2(n) + ilog2(o.beta)));
     const Tables T = tables_of(c);
     const u64* ce_div = ensure_ce_table(c, (int)ilog2(n));
+    static const int MAX_LANES = std::max(1, env_int("XFG_LANES", 2));
+    static const int MIN_PER_LANE = std::max(1, env_int("XFG_MIN_PER_LANE", 8));
     int nl = std::max(1, std::min(MAX_LANES, B / MIN_PER_LANE));
     if (trace_host) nl = 1;
     ensure_lanes(c, nl);
