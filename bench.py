@@ -138,6 +138,7 @@ def main():
     prover = xfgstark.XfgBurnMintProver(device=local_rank)
     n = 1 << args.log_n
     per = args.per_gpu
+    prover.prepare(per, n)  # workspace allocation + code-object load (setup, not a proving step)
 
     call_s = []
 

@@ -99,6 +99,10 @@ int xfg_prove_trace(xfg_ctx* ctx, const uint64_t* trace, uint32_t width, uint64_
 int xfg_prove_batch(xfg_ctx* ctx, uint32_t count, const xfg_burn_inputs* inputs, uint64_t trace_length,
                     const xfg_options* opts, uint8_t* const* outs, size_t* out_lens, int* statuses);
 
+/* allocate every device / pinned-host workspace and load all code objects for batches of
+ * `count` proofs of this shape (setup, not a prove; later calls never allocate) */
+int xfg_prepare(xfg_ctx* ctx, uint32_t count, uint64_t trace_length, const xfg_options* opts);
+
 /* AIR constants from raw inputs (marshalling + Keccak, host); returns a validation status */
 int xfg_burn_air_consts(const xfg_burn_inputs* in, xfg_air_consts* out);
 

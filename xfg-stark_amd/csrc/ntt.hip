@@ -17,6 +17,8 @@
 // Forward LDE output is coset-major: out[p][t][m] = P(7 * w_N^(t + beta*m)), N = beta * n.
 // The coset shift (7 w_N^t)^j, j = C j1 + j2, is split into a pre-factor 7^(C j1) w_(beta R)^(t j1)
 // (LDS table per coset) and a post-factor 7^j2 w_N^(j2 t) folded into the four-step twiddle.
+#include <algorithm>
+#include <cstdlib>
 #include "kernels.hpp"
 
 namespace xfg {
@@ -197,50 +199,44 @@ __global__ __launch_bounds__(THREADS) void ntt_pass_a(NttArgs a) {
     const int TC = 1 << logTC;
     u64* tile = lds;
     u64* ltw = lds + TC * PITCH;
-    u64* pre = ltw + R;  // forward: 7^(C j1) w_(beta R)^(t j1) for the current coset
-    const int poly = blockIdx.y, col0 = blockIdx.x * TC;
+    u64* pre = ltw + R;  // forward: 7^(C j1) w_(beta R)^(t j1) for this block's coset
+    // one block per (column tile, poly, coset); y is [poly][coset][R][C]
+    const int pt = blockIdx.y, col0 = blockIdx.x * TC;
+    const int poly = INV ? pt : (pt >> a.logbeta), t = INV ? 0 : (pt & ((1 << a.logbeta) - 1));
     const u64 n = 1ULL << a.logn;
     const int logN = a.logn + a.logbeta;
     const u64 maskN = (1ULL << logN) - 1;
     for (int i = threadIdx.x; i < R; i += THREADS) {
         ltw[i] = tw_get(a.T, LOGR, i, INV);
-        if (!INV) pre[i] = a.T.pow7[(u64)i << a.logC];
+        if (!INV)
+            pre[i] = gl_mul(a.T.pow7[(u64)i << a.logC],
+                            tw_get(a.T, LOGR + a.logbeta, ((u64)t * i) & ((1ULL << (LOGR + a.logbeta)) - 1), false));
     }
     __syncthreads();
     const u64* in = a.in + (u64)poly * a.in_stride;
-    const int ncos = INV ? 1 : (1 << a.logbeta);
-    for (int t = 0; t < ncos; t++) {
-        if (!INV && t > 0) {
-            // advance pre[j1] from coset t-1 to t: * w_(beta R)^(j1)
-            for (int i = threadIdx.x; i < R; i += THREADS)
-                pre[i] = gl_mul(pre[i], tw_get(a.T, LOGR + a.logbeta, i, false));
-            __syncthreads();
+    u64* y = a.y + (u64)pt * n;
+    auto ldg = [&](int seq, int j1) -> u64 {
+        u64 v = in[((u64)j1 << a.logC) + col0 + seq];
+        return INV ? v : gl_mul(v, pre[j1]);
+    };
+    auto stg = [&](int seq, int base, int stride, u64* v) {
+        const u64 j2 = col0 + seq;
+        u64 w, step;
+        if (INV) {
+            w = tw_get(a.T, a.logn, (j2 * (u64)base) & (n - 1), true);
+            step = tw_get(a.T, a.logn, (j2 * (u64)stride) & (n - 1), true);
+        } else {
+            // 7^j2 w_N^(j2 (t + beta base)); step w_N^(j2 beta stride) = w_n^(j2 stride)
+            w = gl_mul(a.T.pow7[j2], tw_get(a.T, logN, (j2 * ((u64)t + ((u64)base << a.logbeta))) & maskN, false));
+            step = tw_get(a.T, a.logn, (j2 * (u64)stride) & (n - 1), false);
         }
-        u64* y = a.y + ((u64)poly * ncos + t) * n;
-        auto ldg = [&](int seq, int j1) -> u64 {
-            u64 v = in[((u64)j1 << a.logC) + col0 + seq];
-            return INV ? v : gl_mul(v, pre[j1]);
-        };
-        auto stg = [&](int seq, int base, int stride, u64* v) {
-            const u64 j2 = col0 + seq;
-            u64 w, step;
-            if (INV) {
-                w = tw_get(a.T, a.logn, (j2 * (u64)base) & (n - 1), true);
-                step = tw_get(a.T, a.logn, (j2 * (u64)stride) & (n - 1), true);
-            } else {
-                // 7^j2 w_N^(j2 (t + beta base)); step w_N^(j2 beta stride) = w_n^(j2 stride)
-                w = gl_mul(a.T.pow7[j2],
-                           tw_get(a.T, logN, (j2 * ((u64)t + ((u64)base << a.logbeta))) & maskN, false));
-                step = tw_get(a.T, a.logn, (j2 * (u64)stride) & (n - 1), false);
-            }
 #pragma unroll
-            for (int r = 0; r < RR; r++) {
-                y[((u64)(base + r * stride) << a.logC) + j2] = gl_mul(v[r], w);
-                if (r + 1 < RR) w = gl_mul(w, step);
-            }
-        };
-        pass_dft<LOGR, INV, true>(tile, logTC, ltw, ldg, stg);
-    }
+        for (int r = 0; r < RR; r++) {
+            y[((u64)(base + r * stride) << a.logC) + j2] = gl_mul(v[r], w);
+            if (r + 1 < RR) w = gl_mul(w, step);
+        }
+    };
+    pass_dft<LOGR, INV, true>(tile, logTC, ltw, ldg, stg);
 }
 
 // ---------------------------------------------------------------- pass B: row DFTs (size C)
@@ -311,7 +307,7 @@ static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
     const int ncos = inv ? 1 : (1 << a.logbeta);
     size_t lds_a = ((size_t)(1 << logTC) * row_pitch(R) + 2 * R) * sizeof(u64);
     size_t lds_b = ((size_t)(1 << logTR) * row_pitch(C) + C) * sizeof(u64);
-    dim3 ga(C >> logTC, npoly), gb(R >> logTR, npoly * ncos);
+    dim3 ga(C >> logTC, npoly * ncos), gb(R >> logTR, npoly * ncos);
     if (inv) {
         run_pass_a<true>(a.logR, ga, lds_a, s, a);
         run_pass_b<true>(a.logC, gb, lds_b, s, a);
@@ -321,17 +317,34 @@ static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
     }
 }
 
+// The four-step intermediate (beta * n per poly) is produced and consumed chunk by chunk so that
+// it stays resident in the 256 MiB Infinity Cache instead of round-tripping HBM.
+static int lde_chunk(int logn, int logbeta) {
+    const size_t per_poly = (size_t)8 << (logn + logbeta);
+    static const long mb = [] {
+        const char* v = getenv("XFG_LDE_CHUNK_MB");
+        return v && *v ? atol(v) : 0L;
+    }();
+    if (mb <= 0) return 1 << 30;  // no chunking
+    const size_t budget = (size_t)mb << 20;
+    size_t k = budget / per_poly;
+    return k < 1 ? 1 : (int)k;
+}
 void launch_lde(const u64* coef, u64 coef_stride, u64* out, u64* scratch, int npoly, int logn, int logbeta,
                 const Tables& T, hipStream_t s) {
-    NttArgs a{};
-    a.in = coef;
-    a.in_stride = coef_stride;
-    a.y = scratch;
-    a.out = out;
-    a.logn = logn;
-    a.logbeta = logbeta;
-    a.T = T;
-    ntt_run(a, npoly, false, s);
+    const int chunk = lde_chunk(logn, logbeta);
+    const u64 N = 1ULL << (logn + logbeta);
+    for (int p0 = 0; p0 < npoly; p0 += chunk) {
+        NttArgs a{};
+        a.in = coef + (u64)p0 * coef_stride;
+        a.in_stride = coef_stride;
+        a.y = scratch;
+        a.out = out + (u64)p0 * N;
+        a.logn = logn;
+        a.logbeta = logbeta;
+        a.T = T;
+        ntt_run(a, std::min(chunk, npoly - p0), false, s);
+    }
 }
 
 void launch_interpolate(const u64* evals, u64 in_stride, u64* out, u64 out_stride, u64* scratch, int npoly, int logn,

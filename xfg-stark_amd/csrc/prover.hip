@@ -345,8 +345,11 @@ static std::vector<u64> ce_divisor_table(int logn) {
 
 static const char* STAGE_NAMES[] = {"trace_lde",     "trace_commit", "constraint_eval", "composition",
                                     "comp_commit",   "ood",          "deep",            "fri",
-                                    "queries_gather", "host_total"};
-enum { ST_LDE, ST_TCOMMIT, ST_CE, ST_COMP, ST_CCOMMIT, ST_OOD, ST_DEEP, ST_FRI, ST_GATHER, ST_HOST, ST_COUNT };
+                                    "queries_gather", "host_total",  "host_queries",    "host_serialize"};
+enum {
+    ST_LDE, ST_TCOMMIT, ST_CE, ST_COMP, ST_CCOMMIT, ST_OOD, ST_DEEP, ST_FRI, ST_GATHER, ST_HOST, ST_HQUERY, ST_HSER,
+    ST_COUNT
+};
 
 // one lane = one HIP stream + its pooled device buffers + one host thread; a batch is split
 // across lanes so one lane's host-side Fiat-Shamir / serialisation overlaps another's kernels
@@ -458,11 +461,35 @@ struct ProofJob {
 static void stage_mark(Lane* c, int k) {
     if (c->timing) HIPCHK(hipEventRecord(c->ev[k], c->stream));
 }
+// XFG_TRACE=1: host-side phase timestamps of every prove call, printed to stderr
+static bool trace_on() {
+    static const bool on = getenv("XFG_TRACE") && *getenv("XFG_TRACE") == '1';
+    return on;
+}
+struct HostTrace {
+    std::vector<std::pair<const char*, std::chrono::steady_clock::time_point>> m;
+    void mark(const char* what) {
+        if (trace_on()) m.push_back({what, std::chrono::steady_clock::now()});
+    }
+    void dump(int B) {
+        if (!trace_on() || m.size() < 2) return;
+        std::string line = "[xfg] B=" + std::to_string(B);
+        for (size_t i = 1; i < m.size(); i++) {
+            char buf[96];
+            snprintf(buf, sizeof buf, " %s=%.2f", m[i].first,
+                     std::chrono::duration<double, std::milli>(m[i].second - m[i - 1].second).count());
+            line += buf;
+        }
+        fprintf(stderr, "%s\n", line.c_str());
+    }
+};
 
 // the batched prover: jobs[i].air filled; trace_host optional ([B][7][n], else generated on device)
 static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jobs_p, int B, const u64* trace_host,
                        u64 n, const Opts& o) {
     auto t_host0 = std::chrono::steady_clock::now();
+    HostTrace ht;
+    ht.mark("start");
     struct JobSpan {
         ProofJob* p;
         int k;
@@ -510,6 +537,21 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     }
     const u64 rem_len = N >> (3 * nl) >> logbeta;  // D_final / blowup
     c->rem.ensure((size_t)B * std::max<u64>(rem_len, 1));
+    {
+        // opening buffers sized by upper bounds once, so steady-state calls never re-allocate
+        // (hipFree / hipHostMalloc would serialise the device and the other lanes)
+        const size_t q = o.q, depth = logn + logbeta;
+        const size_t vals = (size_t)B * q * (8 + 8 * nl);
+        size_t digs = (size_t)B * q * 2 * depth;
+        for (unsigned l = 0; l < nl; l++) digs += (size_t)B * q * ilog2(D[l] / 8);
+        const size_t opens = (size_t)B * q * 2 * 2 * beta;
+        c->gidx.ensure(vals + digs + (size_t)B * q);
+        c->gval.ensure(vals);
+        c->gdig.ensure(digs + opens);
+        c->h_idx.ensure(vals + digs + (size_t)B * q);
+        c->h_gv.ensure(vals);
+        c->h_gd.ensure(digs + opens);
+    }
 
     AirConst* airs = c->h_air.ensure(B);
     for (int b = 0; b < B; b++) airs[b] = jobs[b].air;
@@ -524,6 +566,7 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     }
 
     // ---- 1. trace LDE + commitment (DefaultTraceLde::new)
+    ht.mark("setup");
     stage_mark(c, 0);
     if (trace_host) HIPCHK(hipMemcpyAsync(c->trace.p, trace_host, (size_t)B * 7 * n * 8, hipMemcpyHostToDevice, s));
     else launch_trace_gen(c->air.p, c->trace.p, logn, B, s);
@@ -534,7 +577,9 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     launch_tree_top(c->tnodes.p, 2 * n, n, B, s);
     Digest* roots = c->h_roots.ensure(B);
     stage_mark(c, 2);
+    ht.mark("launch1");
     fetch_roots(c, c->tnodes.p, 2 * n, B, roots);
+    ht.mark("sync_trace_root");
 
     // ---- 2. constraint composition coefficients (7 transition + 8 boundary)
     u64* co = c->h_co.ensure((size_t)B * 15);
@@ -558,7 +603,9 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     launch_leaves_lde(c->hlde.p, 1, c->hnodes.p, 2 * n, B, logn, logbeta, s);
     launch_tree_top(c->hnodes.p, 2 * n, n, B, s);
     stage_mark(c, 5);
+    ht.mark("launch2");
     fetch_roots(c, c->hnodes.p, 2 * n, B, roots);
+    ht.mark("sync_comp_root");
 
     // ---- 4. OOD point and frame
     const u64 g = gl_root(logn);
@@ -579,7 +626,9 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     u64* ood = c->h_ood.ensure((size_t)B * 15);
     HIPCHK(hipMemcpyAsync(ood, c->ood.p, (size_t)B * 15 * 8, hipMemcpyDeviceToHost, s));
     stage_mark(c, 6);
+    ht.mark("launch3");
     HIPCHK(hipStreamSynchronize(s));
+    ht.mark("sync_ood");
 
     // ---- 5. DEEP composition polynomial (coefficient form) + its LDE
     DeepParams* dps = c->h_dp.ensure(B);
@@ -623,7 +672,9 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         const u64 sstride = cm ? N : D[l];
         launch_fri_leaves(src, sstride, cm, logn, logbeta, rows, c->fnodes[l].p, 2 * rows, B, s);
         launch_tree_top(c->fnodes[l].p, 2 * rows, rows, B, s);
+        ht.mark("fri_launch");
         fetch_roots(c, c->fnodes[l].p, 2 * rows, B, roots);
+        ht.mark("sync_fri");
         for (int b = 0; b < B; b++) {
             auto& j = jobs[b];
             uint8_t rb[32];
@@ -651,8 +702,11 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     u64* dn2h = c->h_dn2.ensure(B);
     HIPCHK(hipMemcpyAsync(dn2h, c->dn2.p, B * 8, hipMemcpyDeviceToHost, s));
     stage_mark(c, 8);
+    ht.mark("launch_rem");
     HIPCHK(hipStreamSynchronize(s));
+    ht.mark("sync_rem");
 
+    auto t_q0 = std::chrono::steady_clock::now();
     // ---- 7. grinding + query positions, gather lists
     // LDE trees store heap levels >= log2(beta) (indices < 2n); lower nodes of an opened row are
     // recomputed by launch_open_rows (local heap: 2 * beta slots per row)
@@ -778,7 +832,11 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     if (ndig + 2 * nopen)
         HIPCHK(hipMemcpyAsync(gd, c->gdig.p, (ndig + 2 * nopen) * sizeof(Digest), hipMemcpyDeviceToHost, s));
     stage_mark(c, 9);
+    auto t_q1 = std::chrono::steady_clock::now();
+    ht.mark("queries_host");
     HIPCHK(hipStreamSynchronize(s));
+    ht.mark("sync_gather");
+    auto t_s0 = std::chrono::steady_clock::now();
 
     // ---- 8. StarkProof::to_bytes (DESIGN.md "Proof format")
     const Digest* open_t = gd + ndig;
@@ -860,14 +918,18 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         w.u64_(j.nonce);
         j.bytes.swap(w.b);
     }
+    ht.mark("serialize");
+    ht.dump(B);
     if (c->timing) {
         for (int k = 0; k < 9; k++) {
             float ms = 0;
             HIPCHK(hipEventElapsedTime(&ms, c->ev[k], c->ev[k + 1]));
             c->stage_ms[k] = ms;
         }
-        c->stage_ms[ST_HOST] =
-            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_host0).count();
+        auto t_end = std::chrono::steady_clock::now();
+        c->stage_ms[ST_HOST] = std::chrono::duration<double, std::milli>(t_end - t_host0).count();
+        c->stage_ms[ST_HQUERY] = std::chrono::duration<double, std::milli>(t_q1 - t_q0).count();
+        c->stage_ms[ST_HSER] = std::chrono::duration<double, std::milli>(t_end - t_s0).count();
     }
 }
 
@@ -899,7 +961,7 @@ static void prove_jobs(xfg_ctx* c, std::vector<ProofJob>& jobs, const u64* trace
     ensure_tables(c, (int)(ilog2(n) + ilog2(o.beta)));
     const Tables T = tables_of(c);
     const u64* ce_div = ensure_ce_table(c, (int)ilog2(n));
-    static const int MAX_LANES = std::max(1, env_int("XFG_LANES", 2));
+    static const int MAX_LANES = std::max(1, env_int("XFG_LANES", 4));
     static const int MIN_PER_LANE = std::max(1, env_int("XFG_MIN_PER_LANE", 8));
     int nl = std::max(1, std::min(MAX_LANES, B / MIN_PER_LANE));
     if (trace_host) nl = 1;
@@ -1114,6 +1176,43 @@ int xfg_prove_batch(xfg_ctx* c, uint32_t count, const xfg_burn_inputs* inputs, u
             statuses[i] = copy_out(c, jobs[k].bytes, outs ? outs[i] : nullptr, &len);
             out_lens[i] = len;
         }
+        return XFG_OK;
+    });
+}
+
+int xfg_prepare(xfg_ctx* c, uint32_t count, uint64_t trace_length, const xfg_options* opts) {
+    if (!c || !opts || count == 0) return XFG_INVALID_ARGUMENT;
+    c->err.clear();
+    u64 n = trace_length ? trace_length : 64;
+    Opts o = to_opts(opts);
+    if (const char* m = check_options(n, o)) {
+        c->err = std::string("Prover error: ") + m;
+        return XFG_PROVER_ERROR;
+    }
+    return guarded(c, [&]() -> int {
+        HIPCHK(hipSetDevice(c->device));
+        // two throw-away proving passes over a fixed valid statement size every lane workspace
+        // (device + pinned host) and load every code object; nothing is cached between proofs
+        xfg_burn_inputs in{};
+        in.burn_amount = in.mint_amount = STANDARD_BURN;
+        for (int i = 0; i < 32; i++) in.tx_prefix_hash[i] = (uint8_t)(i + 1);
+        static const uint8_t rcpt[20] = {1}, sec[32] = {2};
+        in.recipient_address = rcpt;
+        in.recipient_len = 20;
+        in.secret = sec;
+        in.secret_len = 32;
+        in.network_id = 1;
+        in.target_chain_id = 42161;
+        in.commitment_version = 1;
+        AirConst a;
+        std::string err;
+        if (marshal(&in, a, err)) return XFG_PROVER_ERROR;
+        for (int pass = 0; pass < 2; pass++) {
+            std::vector<ProofJob> jobs(count);
+            for (auto& j : jobs) j.air = a;
+            prove_jobs(c, jobs, nullptr, n, o);
+        }
+        HIPCHK(hipDeviceSynchronize());
         return XFG_OK;
     });
 }

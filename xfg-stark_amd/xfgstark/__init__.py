@@ -56,6 +56,7 @@ _lib.xfg_prove_trace.argtypes = [C.c_void_p, _u64p, C.c_uint32, C.c_uint64, C.PO
                                  C.POINTER(_Options), _u8p, C.POINTER(C.c_size_t)]
 _lib.xfg_prove_batch.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(_BurnInputs), C.c_uint64, C.POINTER(_Options),
                                  C.POINTER(_u8p), C.POINTER(C.c_size_t), C.POINTER(C.c_int)]
+_lib.xfg_prepare.argtypes = [C.c_void_p, C.c_uint32, C.c_uint64, C.POINTER(_Options)]
 _lib.xfg_burn_air_consts.argtypes = [C.POINTER(_BurnInputs), C.POINTER(_AirConsts)]
 _lib.xfg_set_timing.argtypes = [C.c_void_p, C.c_int]
 _lib.xfg_stage_times.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_char_p), C.c_int]
@@ -264,6 +265,13 @@ class XfgBurnMintProver:
             else:
                 res.append(StarkProof(C.string_at(base + i * cap, lens[i])))
         return res
+
+    def prepare(self, count, trace_length=64):
+        """allocate workspaces for batches of `count` proofs of this shape (setup, untimed)"""
+        o = self._options._c()
+        st = _lib.xfg_prepare(self._ctx, count, trace_length, C.byref(o))
+        if st:
+            raise self._err(st)
 
     # ---- instrumentation
     def set_timing(self, on=True):
