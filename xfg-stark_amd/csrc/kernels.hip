@@ -56,15 +56,42 @@ __device__ __forceinline__ Digest lde_subtree(const u64* base, u64 n, u64 m, Dig
     }
 }
 
+struct Digest2 {
+    Digest a, b;
+};
+// subtrees of two adjacent LDE rows (m, m+1) over cosets T0 .. T0 + 2^LOG - 1, evaluated depth
+// first: each leaf pair is loaded (one 16-byte load per column) right before it is hashed, so
+// only O(LOGB) digests per row are live
+template <int NC, int LOGB, int LOG, int T0>
+__device__ __forceinline__ Digest2 pair_subtree(const u64* base, u64 n, u64 m) {
+    if constexpr (LOG == 0) {
+        u64 r0[NC], r1[NC];
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(base + ((u64)c * (1 << LOGB) + T0) * n + m);
+            r0[c] = v.x;
+            r1[c] = v.y;
+        }
+        return Digest2{b3_hash_elems<NC>(r0), b3_hash_elems<NC>(r1)};
+    } else {
+        Digest2 l = pair_subtree<NC, LOGB, LOG - 1, T0>(base, n, m);
+        Digest2 r = pair_subtree<NC, LOGB, LOG - 1, T0 + (1 << (LOG - 1))>(base, n, m);
+        return Digest2{b3_merge(l.a, r.a), b3_merge(l.b, r.b)};
+    }
+}
+
+// two consecutive LDE rows per thread: 2 * 2^LOGB leaves, subtree top at level LOGB + 1 =
+// heap node n/2 + m/2
 template <int NC, int LOGB>
 __global__ __launch_bounds__(256) void leaves_lde_kernel(const u64* lde, Digest* nodes_all, u64 node_stride,
                                                          int logn) {
     const u64 n = 1ULL << logn;
     const int proof = blockIdx.y;
-    const u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (m >= n) return;
+    const u64 m2 = (u64)blockIdx.x * blockDim.x + threadIdx.x;  // row pair
+    if (2 * m2 >= n) return;
     const u64* base = lde + (u64)proof * NC * (1 << LOGB) * n;
-    nodes_all[(u64)proof * node_stride + n + m] = lde_subtree<NC, LOGB, LOGB, 0>(base, n, m, nullptr);
+    Digest2 d = pair_subtree<NC, LOGB, LOGB, 0>(base, n, 2 * m2);
+    nodes_all[(u64)proof * node_stride + n / 2 + m2] = b3_merge(d.a, d.b);
 }
 
 // openings: recompute the local subtree heaps of selected rows; entry e = proof << logn | m
@@ -91,7 +118,7 @@ __global__ __launch_bounds__(64) void open_rows_kernel(const u64* lde, const u64
 void launch_leaves_lde(const u64* lde, int nc, Digest* nodes, u64 node_stride, int npoly, int logn, int logbeta,
                        hipStream_t s) {
     u64 n = 1ULL << logn;
-    dim3 g((unsigned)((n + 255) / 256), npoly), b(256);
+    dim3 g((unsigned)((n / 2 + 255) / 256), npoly), b(256);
     if (nc == 7) { XFG_LOGB_DISPATCH(leaves_lde_kernel, 7, logbeta, g, b, 0, s, lde, nodes, node_stride, logn) }
     else { XFG_LOGB_DISPATCH(leaves_lde_kernel, 1, logbeta, g, b, 0, s, lde, nodes, node_stride, logn) }
     XFG_CHECK_LAUNCH();
@@ -155,7 +182,8 @@ void launch_tree_top(Digest* nodes, u64 node_stride, u64 count, int npoly, hipSt
     while (count > 512) {
         int lg = 0;
         while ((1ULL << (lg + 1)) <= count) lg++;
-        int h = lg - 9 < 3 ? lg - 9 : 3;
+        int h = 1;  // one coalesced merge per thread per level (multi-level variants gather 2^h
+                    // digests per lane uncoalesced and measured slower)
         u64 outc = count >> h;
         dim3 g((unsigned)((outc + 255) / 256), npoly);
         if (h == 3) hipLaunchKernelGGL(tree_up_kernel<3>, g, dim3(256), 0, s, nodes, node_stride, count);

@@ -41,7 +41,8 @@ void launch_interpolate(const u64* evals, u64 in_stride, u64* out, u64 out_strid
                         bool off7, u64 keep, const Tables& T, hipStream_t s);
 
 // ---- Merkle (heap layout: nodes[1] = root, nodes[L + i] = leaf i) ----
-// LDE commitments store levels >= log2(beta) only: node_stride >= 2n, top of row m at n + m
+// LDE commitments store levels >= log2(beta) + 1 only: node_stride >= 2n; the subtree over rows
+// (2j, 2j+1) tops out at heap node n/2 + j; launch_tree_top(nodes, stride, n / 2, ...) finishes
 void launch_leaves_lde(const u64* lde, int nc, Digest* nodes, u64 node_stride, int npoly, int logn, int logbeta,
                        hipStream_t s);
 // recompute the local subtree heap (2 * beta digests, slot 1 = top, leaf t at beta + t) of LDE

@@ -544,11 +544,11 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         const size_t vals = (size_t)B * q * (8 + 8 * nl);
         size_t digs = (size_t)B * q * 2 * depth;
         for (unsigned l = 0; l < nl; l++) digs += (size_t)B * q * ilog2(D[l] / 8);
-        const size_t opens = (size_t)B * q * 2 * 2 * beta;
-        c->gidx.ensure(vals + digs + (size_t)B * q);
+        const size_t opens = (size_t)B * q * 2 * 2 * 2 * beta;
+        c->gidx.ensure(vals + digs + (size_t)B * 2 * q);
         c->gval.ensure(vals);
         c->gdig.ensure(digs + opens);
-        c->h_idx.ensure(vals + digs + (size_t)B * q);
+        c->h_idx.ensure(vals + digs + (size_t)B * 2 * q);
         c->h_gv.ensure(vals);
         c->h_gd.ensure(digs + opens);
     }
@@ -574,7 +574,7 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     launch_lde(c->coef.p, n, c->lde.p, c->scratch.p, B * 7, logn, logbeta, T, s);
     stage_mark(c, 1);
     launch_leaves_lde(c->lde.p, 7, c->tnodes.p, 2 * n, B, logn, logbeta, s);
-    launch_tree_top(c->tnodes.p, 2 * n, n, B, s);
+    launch_tree_top(c->tnodes.p, 2 * n, n / 2, B, s);
     Digest* roots = c->h_roots.ensure(B);
     stage_mark(c, 2);
     ht.mark("launch1");
@@ -601,7 +601,7 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     launch_lde(c->hcoef.p, n, c->hlde.p, c->scratch.p, B, logn, logbeta, T, s);
     stage_mark(c, 4);
     launch_leaves_lde(c->hlde.p, 1, c->hnodes.p, 2 * n, B, logn, logbeta, s);
-    launch_tree_top(c->hnodes.p, 2 * n, n, B, s);
+    launch_tree_top(c->hnodes.p, 2 * n, n / 2, B, s);
     stage_mark(c, 5);
     ht.mark("launch2");
     fetch_roots(c, c->hnodes.p, 2 * n, B, roots);
@@ -710,7 +710,7 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     // ---- 7. grinding + query positions, gather lists
     // LDE trees store heap levels >= log2(beta) (indices < 2n); lower nodes of an opened row are
     // recomputed by launch_open_rows (local heap: 2 * beta slots per row)
-    const u64 stored_lim = 2 * n, LB = beta;
+    const u64 stored_lim = n, LB = beta;  // stored: heap levels >= log2(beta) + 1
     std::vector<u64> vidx_lde, vidx_h, didx_t, didx_h, open_ent;
     std::vector<std::vector<u64>> vidx_f(nl + 1), didx_f(nl + 1);
     struct Layout {
@@ -748,10 +748,15 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
             for (int col = 0; col < 7; col++) vidx_lde.push_back((((u64)b * 7 + col) * beta + t) * n + m);
             vidx_h.push_back(((u64)b * beta + t) * n + m);
         }
-        // rows whose subtrees are recomputed: positions are sorted, so rows come sorted
+        // rows whose subtrees are recomputed: every queried row and its sibling row (the sibling's
+        // subtree top, heap level log2(beta), is no longer stored)
         std::vector<u64> rows_b;
-        for (u64 k : pos)
-            if (rows_b.empty() || rows_b.back() != (k >> logbeta)) rows_b.push_back(k >> logbeta);
+        for (u64 k : pos) {
+            rows_b.push_back(k >> logbeta);
+            rows_b.push_back((k >> logbeta) ^ 1);
+        }
+        std::sort(rows_b.begin(), rows_b.end());
+        rows_b.erase(std::unique(rows_b.begin(), rows_b.end()), rows_b.end());
         const u64 ent0 = open_ent.size();
         for (u64 m : rows_b) open_ent.push_back(((u64)b << logn) | m);
         L.op = plan_batch_opening(pos, N);
@@ -759,8 +764,8 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         for (auto& v : L.op.vecs)
             for (u64 h : v) {
                 if (h < stored_lim) {
-                    didx_t.push_back((u64)b * stored_lim + h);
-                    didx_h.push_back((u64)b * stored_lim + h);
+                    didx_t.push_back((u64)b * 2 * n + h);
+                    didx_h.push_back((u64)b * 2 * n + h);
                     L.ref.push_back(stored_ord++);
                 } else {
                     unsigned lvl = (unsigned)(logn + logbeta) - (63 - __builtin_clzll(h));  // 0 = leaves
