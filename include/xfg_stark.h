@@ -24,7 +24,8 @@
  * Output bytes are the proof's `StarkProof::to_bytes()` serialisation as restated in DESIGN.md
  * ("Proof format"); the caller owns all host buffers, the library owns device memory (pooled per
  * context). `out == NULL` (or *out_len too small) returns the required size in *out_len.
- * A context is bound to one HIP device and one stream; use one context per thread.
+ * A context is bound to one HIP device; it owns XFG_LANES (default 4) lanes, each a HIP stream with
+ * its workspace and a host worker thread. Submit from one thread per context.
  */
 #ifndef XFG_STARK_H
 #define XFG_STARK_H
@@ -98,6 +99,17 @@ int xfg_prove_trace(xfg_ctx* ctx, const uint64_t* trace, uint32_t width, uint64_
  * the batch ran (individual proofs may still carry validation errors) */
 int xfg_prove_batch(xfg_ctx* ctx, uint32_t count, const xfg_burn_inputs* inputs, uint64_t trace_length,
                     const xfg_options* opts, uint8_t* const* outs, size_t* out_lens, int* statuses);
+
+/* asynchronous form of xfg_prove_batch for pipelined callers (a proving service, bench.py):
+ * inputs are validated and marshalled before this returns (statuses[i] of invalid inputs are set
+ * now); outs / out_lens / statuses must stay valid until xfg_batch_wait(ticket) returns. Batches
+ * submitted back to back share the context's lane workers, so the host-side tail of one (query
+ * openings, serialisation) overlaps the kernels of the next. */
+int xfg_prove_batch_submit(xfg_ctx* ctx, uint32_t count, const xfg_burn_inputs* inputs, uint64_t trace_length,
+                           const xfg_options* opts, uint8_t* const* outs, size_t* out_lens, int* statuses,
+                           uint64_t* ticket);
+/* blocks until the batch is proven and its outputs written; returns like xfg_prove_batch */
+int xfg_batch_wait(xfg_ctx* ctx, uint64_t ticket);
 
 /* allocate every device / pinned-host workspace and load all code objects for batches of
  * `count` proofs of this shape (setup, not a prove; later calls never allocate) */

@@ -1,0 +1,54 @@
+// Microbenchmark: wave64 issue throughput of the integer VALU instructions used by BLAKE3 and the
+// Goldilocks field code on gfx950 (8 independent chains per lane, 8 waves per SIMD)
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#define REP8(X) X X X X X X X X
+#define DEF(NAME, ASM)                                                                           \
+    __global__ __launch_bounds__(256) void NAME(unsigned* out, int iters) {                    \
+        unsigned a0 = threadIdx.x, a1 = a0 * 3, a2 = a0 * 5, a3 = a0 * 7, a4 = a0 + 1, a5 = a0 + 2, \
+                 a6 = a0 + 3, a7 = a0 + 4, k = blockIdx.x | 1;                                  \
+        for (int it = 0; it < iters; it++) {                                                     \
+            REP8(asm volatile(ASM : "+v"(a0) : "v"(k)); asm volatile(ASM : "+v"(a1) : "v"(k));   \
+                 asm volatile(ASM : "+v"(a2) : "v"(k)); asm volatile(ASM : "+v"(a3) : "v"(k));   \
+                 asm volatile(ASM : "+v"(a4) : "v"(k)); asm volatile(ASM : "+v"(a5) : "v"(k));   \
+                 asm volatile(ASM : "+v"(a6) : "v"(k)); asm volatile(ASM : "+v"(a7) : "v"(k));)  \
+        }                                                                                        \
+        out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;       \
+    }
+DEF(k_add, "v_add_u32 %0, %0, %1")
+DEF(k_xor, "v_xor_b32 %0, %0, %1")
+DEF(k_add3, "v_add3_u32 %0, %0, %1, %0")
+DEF(k_alignbit, "v_alignbit_b32 %0, %0, %0, 16")
+DEF(k_xad, "v_xad_u32 %0, %0, %1, %0")
+DEF(k_bitop3, "v_bitop3_b32 %0, %0, %1, %0 bitop3:0x96")
+DEF(k_perm, "v_perm_b32 %0, %0, %1, %1")
+DEF(k_mad32, "v_mad_u32_u24 %0, %0, %1, %0")
+DEF(k_mullo, "v_mul_lo_u32 %0, %0, %1")
+DEF(k_mulhi, "v_mul_hi_u32 %0, %0, %1")
+DEF(k_addco, "v_add_co_u32 %0, vcc, %0, %1")
+DEF(k_lshl_or, "v_lshl_or_b32 %0, %0, 7, %1")
+int main() {
+    unsigned* d;
+    const int blocks = 256 * 8, threads = 256, iters = 256;
+    hipMalloc(&d, (size_t)blocks * threads * 4);
+    struct { const char* n; void (*f)(unsigned*, int); } ks[] = {
+        {"v_add_u32", k_add}, {"v_xor_b32", k_xor}, {"v_add3_u32", k_add3}, {"v_alignbit_b32", k_alignbit},
+        {"v_xad_u32", k_xad}, {"v_bitop3_b32", k_bitop3}, {"v_perm_b32", k_perm}, {"v_mad_u32_u24", k_mad32},
+        {"v_mul_lo_u32", k_mullo}, {"v_mul_hi_u32", k_mulhi}, {"v_add_co_u32", k_addco}, {"v_lshl_or_b32", k_lshl_or}};
+    for (auto& k : ks) {
+        hipEvent_t a, b;
+        hipEventCreate(&a);
+        hipEventCreate(&b);
+        float ms = 0;
+        for (int rep = 0; rep < 2; rep++) {
+            hipEventRecord(a);
+            hipLaunchKernelGGL(k.f, dim3(blocks), dim3(threads), 0, 0, d, iters);
+            hipEventRecord(b);
+            hipEventSynchronize(b);
+            hipEventElapsedTime(&ms, a, b);
+        }
+        double ops = (double)blocks * threads * iters * 64;
+        printf("%-16s %.3f ms  %.1f T lane-ops/s\n", k.n, ms, ops / ms / 1e9);
+    }
+    return 0;
+}

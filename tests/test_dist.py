@@ -22,7 +22,7 @@ def _fake_prove(kws):
     return out
 
 
-def _worker(rank, world, port, per, ret):
+def _worker(rank, world, port, per, ret, mode="sync"):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     for p in (os.path.join(root, "xfg-stark_amd"), root):
@@ -34,8 +34,24 @@ def _worker(rank, world, port, per, ret):
     import bench
     import synthetic
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    inputs = [synthetic.burn_inputs(i) for i in range(per * world)] if rank == 0 else None
-    out = bench.sharded_step(_fake_prove, inputs, rank, world, per, torch.device("cpu"), dist)
+    if mode == "sync":
+        inputs = [synthetic.burn_inputs(i) for i in range(per * world)] if rank == 0 else None
+        out = bench.sharded_step(_fake_prove, inputs, rank, world, per, torch.device("cpu"), dist)
+    else:
+        # bench.py's timed loop: 3 steps, submission depth 2, inputs pre-packed on rank 0
+        batches = [[synthetic.burn_inputs(100 * k + i) for i in range(per * world)] if rank == 0 else None
+                   for k in range(3)]
+        packed = [torch.from_numpy(bench.pack_inputs(b)).view(world, per, bench.REC) if rank == 0 else None
+                  for b in batches]
+        seen = []
+
+        def submit(kws):
+            seen.append(len(kws))
+            return _fake_prove(kws)
+
+        out = bench.pipelined_steps(submit, lambda p: p, batches, rank, world, per, torch.device("cpu"), dist,
+                                    packed)
+        assert seen == [per] * 3
     if rank == 0:
         ret.put(out)
     else:
@@ -52,20 +68,21 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("world,per", [(2, 3), (2, 1)])
-def test_sharded_step_gloo(world, per):
+@pytest.mark.parametrize("world,per,mode", [(2, 3, "sync"), (2, 1, "sync"), (2, 2, "pipelined")])
+def test_sharded_step_gloo(world, per, mode):
     import synthetic
     ctx = mp.get_context("spawn")
     ret = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, per, ret)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, per, ret, mode)) for r in range(world)]
     for p in procs:
         p.start()
     out = ret.get(timeout=120)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    want = _fake_prove([synthetic.burn_inputs(i) for i in range(per * world)])
+    base = 200 if mode == "pipelined" else 0  # pipelined: the last of 3 steps
+    want = _fake_prove([synthetic.burn_inputs(base + i) for i in range(per * world)])
     assert out == want
 
 

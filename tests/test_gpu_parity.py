@@ -100,6 +100,25 @@ def test_batch_equals_oracle_per_proof(prover):
         assert pr.to_bytes() == want
 
 
+def test_submitted_batches_in_flight_match_oracle(prover):
+    """xfg_prove_batch_submit: three batches (different trace lengths, one spanning several lane
+    units) in flight together, collected out of order; every proof equals the oracle's."""
+    import xfgstark
+    with_blowup(prover, 8)
+    plan = [(1024, [synthetic.burn_inputs(300 + i) for i in range(40)]),
+            (256, [synthetic.burn_inputs(400 + i) for i in range(5)]),
+            (2048, [synthetic.burn_inputs(500 + i) for i in range(3)])]
+    pend = [prover.submit_batch(kws, trace_length=n) for n, kws in plan]
+    with pytest.raises(xfgstark.XfgStarkError):  # lane 0 belongs to the workers meanwhile
+        prover.debug_lde(np.zeros((1, 8), dtype=np.uint64), 8, 2)
+    for (n, kws), pb in reversed(list(zip(plan, pend))):
+        res = pb.result()
+        assert len(res) == len(kws)
+        for kw, pr in zip(kws, res):
+            st, want = O.prove(oracle_air(kw), n, O.options())
+            assert st == 0 and pr.to_bytes() == want
+
+
 def test_batch_isolates_invalid_inputs(prover):
     import xfgstark
     with_blowup(prover, 8)

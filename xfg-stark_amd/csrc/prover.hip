@@ -16,6 +16,9 @@
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <mutex>
+#include <condition_variable>
+#include <deque>
 #include <vector>
 
 #include "../../include/xfg_stark.h"
@@ -207,17 +210,29 @@ static int marshal(const xfg_burn_inputs* in, AirConst& a, std::string& err) {
 // ------------------------------------------------------------------ byte writer
 struct BW {
     std::vector<uint8_t> b;
-    void put(const void* p, size_t k) {
-        size_t o = b.size();
-        b.resize(o + k);
-        memcpy(b.data() + o, p, k);
+    size_t o = 0;
+    uint8_t* at(size_t k) {  // k bytes at the cursor (grows geometrically; callers pre-size)
+        if (o + k > b.size()) b.resize(std::max(2 * b.size(), o + k));
+        uint8_t* q = b.data() + o;
+        o += k;
+        return q;
     }
-    void u8(u64 v) { b.push_back((uint8_t)v); }
+    void put(const void* p, size_t k) { memcpy(at(k), p, k); }
+    void u8(u64 v) { *at(1) = (uint8_t)v; }
     void u16(u64 v) { uint16_t x = (uint16_t)v; put(&x, 2); }  // little-endian host
     void u32(u64 v) { uint32_t x = (uint32_t)v; put(&x, 4); }
     void u64_(u64 v) { put(&v, 8); }
     void u64s(const u64* v, size_t k) { put(v, 8 * k); }
     void digest(const Digest& d) { put(d.w, 32); }  // LE words == digest bytes
+    size_t len_slot() { at(4); return o; }          // u32 byte length of what follows
+    void len_patch(size_t end_of_slot) {
+        uint32_t x = (uint32_t)(o - end_of_slot);
+        memcpy(b.data() + end_of_slot - 4, &x, 4);
+    }
+    void finish(std::vector<uint8_t>& out) {
+        b.resize(o);
+        out.swap(b);
+    }
 };
 
 // ------------------------------------------------------------------ batch Merkle openings
@@ -225,38 +240,54 @@ struct BW {
 // the missing sibling leaf of normalised pair i, then the siblings met by the i-th entry of each
 // upper level's index list. Digests are gathered from HBM afterwards in this order.
 struct BatchOpening {
-    std::vector<std::vector<u64>> vecs;  // heap indices (leaf i -> L + i)
+    // node vector i = node[i * stride .. i * stride + len[i]) (heap indices, leaf i -> L + i)
+    u64 stride = 0;
+    std::vector<u64> node;
+    std::vector<uint8_t> len;
+    size_t size() const { return len.size(); }
+    const u64* row(size_t i) const { return node.data() + i * stride; }
+    template <class F>
+    void each(F f) const {
+        for (size_t i = 0; i < len.size(); i++)
+            for (unsigned k = 0; k < len[i]; k++) f(node[i * stride + k]);
+    }
 };
-static BatchOpening plan_batch_opening(const std::vector<u64>& idx, u64 L) {
+static void plan_batch_opening(const std::vector<u64>& idx, u64 L, BatchOpening& op) {
     unsigned depth = ilog2(L);
-    std::vector<u64> norm;
-    for (u64 i : idx) norm.push_back(i & ~1ULL);
-    std::sort(norm.begin(), norm.end());
-    norm.erase(std::unique(norm.begin(), norm.end()), norm.end());
-    BatchOpening op;
-    op.vecs.resize(norm.size());
-    std::vector<u64> cur(norm.size());
-    for (size_t i = 0; i < norm.size(); i++) {
-        for (u64 leaf = norm[i]; leaf < norm[i] + 2; leaf++)
-            if (std::find(idx.begin(), idx.end(), leaf) == idx.end()) op.vecs[i].push_back(L + leaf);
-        cur[i] = (norm[i] + L) >> 1;
+    u64 cur[256], sorted[256];  // idx.size() <= num_queries <= 255
+    size_t cnt = idx.size();
+    std::copy(idx.begin(), idx.end(), sorted);
+    std::sort(sorted, sorted + cnt);
+    size_t nn = 0;
+    for (size_t i = 0; i < cnt; i++) {
+        u64 v = sorted[i] & ~1ULL;
+        if (nn == 0 || cur[nn - 1] != v) cur[nn++] = v;
+    }
+    op.stride = depth + 1;
+    op.len.assign(nn, 0);
+    op.node.resize(nn * op.stride);
+    auto push = [&](size_t i, u64 h) { op.node[i * op.stride + op.len[i]++] = h; };
+    for (size_t i = 0; i < nn; i++) {
+        for (u64 leaf = cur[i]; leaf < cur[i] + 2; leaf++)
+            if (!std::binary_search(sorted, sorted + cnt, leaf)) push(i, L + leaf);
+        cur[i] = (cur[i] + L) >> 1;
     }
     for (unsigned lvl = 1; lvl < depth; lvl++) {
-        std::vector<u64> nxt;
-        for (size_t i = 0; i < cur.size(); i++) {
+        size_t m = 0;
+        for (size_t i = 0; i < nn; i++) {
             u64 sib = cur[i] ^ 1;
-            if (i + 1 < cur.size() && cur[i + 1] == sib) i++;
-            else op.vecs[i].push_back(sib);
-            nxt.push_back(sib >> 1);
+            if (i + 1 < nn && cur[i + 1] == sib) i++;
+            else push(i, sib);
+            cur[m++] = sib >> 1;  // m <= i: in-place compaction is safe
         }
-        cur.swap(nxt);
+        nn = m;
     }
-    return op;
 }
 static std::vector<u64> fold_positions(const std::vector<u64>& in, u64 target) {
     std::vector<u64> out;
+    out.reserve(in.size());
     for (u64 p : in) {
-        u64 q = p % target;
+        u64 q = p & (target - 1);  // target is a power of two
         if (std::find(out.begin(), out.end(), q) == out.end()) out.push_back(q);
     }
     return out;
@@ -310,8 +341,7 @@ struct HBuf {
 struct TablesHost {
     int LM = -1;
     DBuf<u64> tw, pow7, ipow7;
-    int ce_logn = -1;
-    DBuf<u64> ce_div;  // constraint divisor table for trace length 2^ce_logn
+    std::map<int, DBuf<u64>> ce_div;  // constraint divisor tables per log2(trace length)
 };
 
 // Data-independent constraint divisors on the CE domain x_i = 7 w_2n^i (i = 2m + par), laid out
@@ -388,12 +418,31 @@ struct Lane {
 
 }  // namespace xfg
 
+namespace xfg {
+struct Batch;
+struct Unit {
+    Batch* b;
+    int b0, b1;
+    int lane;  // -1: any worker
+};
+}  // namespace xfg
+
 struct xfg_ctx {
     int device = 0;
     std::string err;
     bool timing = false;
     xfg::TablesHost tables;
     std::vector<std::unique_ptr<xfg::Lane>> lanes;
+    // persistent lane workers: one host thread per lane pulls proof units from a FIFO shared by
+    // every submitted batch, so the host tail of one batch overlaps the kernels of the next
+    std::mutex qm;
+    std::condition_variable qcv, dcv;
+    std::deque<xfg::Unit> q;
+    std::vector<std::thread> workers;
+    bool stop = false;
+    uint64_t next_ticket = 1;
+    std::map<uint64_t, std::unique_ptr<xfg::Batch>> pending;
+    int last_lane = 0;
 };
 
 namespace xfg {
@@ -423,13 +472,13 @@ static void ensure_tables(xfg_ctx* c, int LM) {
     c->tables.LM = LM;
 }
 static const u64* ensure_ce_table(xfg_ctx* c, int logn) {
-    if (c->tables.ce_logn != logn) {
+    auto& d = c->tables.ce_div[logn];
+    if (!d.p) {
         std::vector<u64> t = ce_divisor_table(logn);
-        c->tables.ce_div.ensure(t.size());
-        HIPCHK(hipMemcpy(c->tables.ce_div.p, t.data(), t.size() * 8, hipMemcpyHostToDevice));
-        c->tables.ce_logn = logn;
+        d.ensure(t.size());
+        HIPCHK(hipMemcpy(d.p, t.data(), t.size() * 8, hipMemcpyHostToDevice));
     }
-    return c->tables.ce_div.p;
+    return d.p;
 }
 static Tables tables_of(xfg_ctx* c) {
     Tables T;
@@ -468,6 +517,18 @@ static bool trace_on() {
 }
 struct HostTrace {
     std::vector<std::pair<const char*, std::chrono::steady_clock::time_point>> m;
+    std::map<std::string, double> acc;  // accumulated sub-phase ms
+    using clk = std::chrono::steady_clock;
+    clk::time_point t_ = {};
+    void tic() {
+        if (trace_on()) t_ = clk::now();
+    }
+    void toc(const char* what) {
+        if (!trace_on()) return;
+        auto t = clk::now();
+        acc[what] += std::chrono::duration<double, std::milli>(t - t_).count();
+        t_ = t;
+    }
     void mark(const char* what) {
         if (trace_on()) m.push_back({what, std::chrono::steady_clock::now()});
     }
@@ -478,6 +539,11 @@ struct HostTrace {
             char buf[96];
             snprintf(buf, sizeof buf, " %s=%.2f", m[i].first,
                      std::chrono::duration<double, std::milli>(m[i].second - m[i - 1].second).count());
+            line += buf;
+        }
+        for (auto& kv : acc) {
+            char buf[96];
+            snprintf(buf, sizeof buf, " [%s=%.3f]", kv.first.c_str(), kv.second);
             line += buf;
         }
         fprintf(stderr, "%s\n", line.c_str());
@@ -722,6 +788,7 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     std::vector<Layout> lay(B);
     for (int b = 0; b < B; b++) {
         auto& j = jobs[b];
+        ht.tic();
         if (dn2h[b] == 0) j.status = XFG_PROVER_ERROR;  // assert_eq!(trace_length - 2, degree)
         Digest rc = hash_elements(&remh[(size_t)b * rem_len], rem_len);
         uint8_t rb[32];
@@ -742,6 +809,7 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         std::sort(pos.begin(), pos.end());
         pos.erase(std::unique(pos.begin(), pos.end()), pos.end());
         j.pos = pos;
+        ht.toc("q_grind_draw");
         Layout& L = lay[b];
         for (u64 k : pos) {
             u64 t = k & (beta - 1), m = k >> logbeta;
@@ -759,10 +827,9 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         rows_b.erase(std::unique(rows_b.begin(), rows_b.end()), rows_b.end());
         const u64 ent0 = open_ent.size();
         for (u64 m : rows_b) open_ent.push_back(((u64)b << logn) | m);
-        L.op = plan_batch_opening(pos, N);
+        plan_batch_opening(pos, N, L.op);
         int64_t stored_ord = 0;
-        for (auto& v : L.op.vecs)
-            for (u64 h : v) {
+        L.op.each([&](u64 h) {
                 if (h < stored_lim) {
                     didx_t.push_back((u64)b * 2 * n + h);
                     didx_h.push_back((u64)b * 2 * n + h);
@@ -774,7 +841,8 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
                     u64 e = ent0 + (std::lower_bound(rows_b.begin(), rows_b.end(), m) - rows_b.begin());
                     L.ref.push_back(-(int64_t)(e * 2 * LB + local) - 1);
                 }
-            }
+            });
+        ht.toc("q_lde_plan");
         std::vector<u64> fp = pos;
         for (unsigned l = 0; l < nl; l++) {
             u64 rows = D[l] / 8;
@@ -786,10 +854,13 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
                     if (l == 0) vidx_f[0].push_back(((u64)b * beta + (K & (beta - 1))) * n + (K >> logbeta));
                     else vidx_f[l].push_back((u64)b * D[l] + K);
                 }
-            L.fops.push_back(plan_batch_opening(fp, rows));
-            for (auto& v : L.fops.back().vecs) for (u64 x : v) didx_f[l].push_back((u64)b * 2 * rows + x);
+            L.fops.emplace_back();
+            plan_batch_opening(fp, rows, L.fops.back());
+            L.fops.back().each([&](u64 x) { didx_f[l].push_back((u64)b * 2 * rows + x); });
         }
+        ht.toc("q_fri_plan");
     }
+    ht.mark("queries_plan");
     // one index buffer, one value buffer, one digest buffer; segment per source
     std::vector<u64> allidx;
     std::vector<std::pair<size_t, size_t>> vseg, dseg;  // (offset, count)
@@ -855,35 +926,34 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         for (unsigned l = 0; l < nl; l++) { cur_fd[l] = off; off += didx_f[l].size(); }
     }
     auto write_paths = [&](BW& w, const BatchOpening& op, size_t& cursor) {
-        BW p;
-        p.u8(op.vecs.size());
-        for (auto& v : op.vecs) {
-            p.u8(v.size());
-            p.put(&gd[cursor], 32 * v.size());
-            cursor += v.size();
+        size_t slot = w.len_slot();
+        w.u8(op.size());
+        for (size_t i = 0; i < op.size(); i++) {
+            w.u8(op.len[i]);
+            w.put(&gd[cursor], 32 * op.len[i]);
+            cursor += op.len[i];
         }
-        w.u32(p.b.size());
-        w.put(p.b.data(), p.b.size());
+        w.len_patch(slot);
     };
     auto write_lde_paths = [&](BW& w, const Layout& L, size_t& cursor, const Digest* open) {
-        BW p;
-        p.u8(L.op.vecs.size());
+        size_t slot = w.len_slot();
+        w.u8(L.op.size());
         size_t r = 0;
-        for (auto& v : L.op.vecs) {
-            p.u8(v.size());
-            for (size_t k = 0; k < v.size(); k++, r++) {
+        for (size_t i = 0; i < L.op.size(); i++) {
+            w.u8(L.op.len[i]);
+            uint8_t* q = w.at(32 * L.op.len[i]);
+            for (size_t k = 0; k < L.op.len[i]; k++, r++) {
                 int64_t ref = L.ref[r];
-                p.digest(ref >= 0 ? gd[cursor++] : open[-ref - 1]);
+                memcpy(q + 32 * k, (ref >= 0 ? gd[cursor++] : open[-ref - 1]).w, 32);
             }
         }
-        w.u32(p.b.size());
-        w.put(p.b.data(), p.b.size());
+        w.len_patch(slot);
     };
     for (int b = 0; b < B; b++) {
         auto& j = jobs[b];
         const u64 nu = j.pos.size();
         BW w;
-        w.b.reserve(j.commitments.size() + nu * 8 * (8 + 8 * nl) + (2 + nl) * nu * 32 * ilog2(N) + 1024);
+        w.b.resize(j.commitments.size() + nu * 8 * (8 + 8 * nl) + (2 + nl) * nu * 32 * ilog2(N) + 1024);
         // Context
         w.u8(7); w.u8(0); w.u8(logn); w.u16(0);
         w.u8(8); w.u64_(P);
@@ -921,7 +991,7 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         for (u64 i = 0; i < rem_len; i++) w.u64_(remh[(size_t)b * rem_len + i]);
         w.u8(0);
         w.u64_(j.nonce);
-        j.bytes.swap(w.b);
+        w.finish(j.bytes);
     }
     ht.mark("serialize");
     ht.dump(B);
@@ -954,46 +1024,173 @@ static void ensure_lanes(xfg_ctx* c, size_t k) {
         for (auto& e : c->lanes.back()->ev) HIPCHK(hipEventCreate(&e));
     }
 }
-// proofs per lane below which a batch is not split (each lane runs a full pipeline); overridable
-// with XFG_LANES / XFG_MIN_PER_LANE for tuning
+// lane / work-unit tuning knobs (XFG_LANES, XFG_UNIT)
 static int env_int(const char* name, int dflt) {
     const char* v = getenv(name);
     return v && *v ? atoi(v) : dflt;
 }
 
-static void prove_jobs(xfg_ctx* c, std::vector<ProofJob>& jobs, const u64* trace_host, u64 n, const Opts& o) {
-    const int B = (int)jobs.size();
-    ensure_tables(c, (int)(ilog2(n) + ilog2(o.beta)));
-    const Tables T = tables_of(c);
-    const u64* ce_div = ensure_ce_table(c, (int)ilog2(n));
-    static const int MAX_LANES = std::max(1, env_int("XFG_LANES", 4));
-    static const int MIN_PER_LANE = std::max(1, env_int("XFG_MIN_PER_LANE", 8));
-    int nl = std::max(1, std::min(MAX_LANES, B / MIN_PER_LANE));
-    if (trace_host) nl = 1;
-    ensure_lanes(c, nl);
-    for (auto& L : c->lanes) L->timing = c->timing;
-    if (nl == 1) {
-        prove_lane(c->lanes[0].get(), T, ce_div, jobs.data(), B, trace_host, n, o);
-        return;
+// ------------------------------------------------------------------ batch submission / lane workers
+// a submitted batch: jobs [0, B) proven in units of XFG_UNIT proofs by the lane workers; proof
+// bytes are copied into the caller's buffers on the worker thread as each unit finishes
+struct Batch {
+    std::vector<ProofJob> jobs;
+    std::vector<uint32_t> which;   // jobs[k] -> caller index
+    std::vector<uint8_t*> outs;    // caller buffers (null entry or empty: size query)
+    size_t* out_lens = nullptr;    // caller capacities in, proof lengths out
+    int* statuses = nullptr;       // caller statuses, written by wait
+    std::vector<int> st;           // per-job copy-out status
+    const u64* trace_host = nullptr;
+    u64 n = 0;
+    Opts o{};
+    Tables T{};
+    const u64* ce_div = nullptr;
+    int units_left = 0;
+    std::exception_ptr err;
+};
+
+static int max_lanes() {
+    static const int v = std::max(1, env_int("XFG_LANES", 4));
+    return v;
+}
+static int unit_size() {
+    static const int v = std::max(1, env_int("XFG_UNIT", 16));
+    return v;
+}
+
+static void copy_unit(Batch* b, int b0, int b1) {
+    for (int k = b0; k < b1; k++) {
+        ProofJob& j = b->jobs[k];
+        if (j.status) {
+            b->st[k] = j.status;
+            continue;
+        }
+        if (b->which.empty()) {  // warm-up batch (xfg_prepare): bytes discarded
+            std::vector<uint8_t>().swap(j.bytes);
+            continue;
+        }
+        uint32_t i = b->which[k];
+        size_t need = j.bytes.size();
+        uint8_t* dst = b->outs.empty() ? nullptr : b->outs[i];
+        if (!dst) {
+            b->st[k] = XFG_OK;  // size query (copy_out semantics)
+        } else if (b->out_lens[i] >= need) {
+            memcpy(dst, j.bytes.data(), need);
+            b->st[k] = XFG_OK;
+        } else {
+            b->st[k] = XFG_BUFFER_TOO_SMALL;
+        }
+        b->out_lens[i] = need;
+        std::vector<uint8_t>().swap(j.bytes);
     }
-    std::vector<std::thread> th;
-    std::vector<std::exception_ptr> errs(nl);
-    int per = (B + nl - 1) / nl;
-    for (int l = 0; l < nl; l++) {
-        int b0 = l * per, b1 = std::min(B, b0 + per);
-        if (b0 >= b1) break;
-        th.emplace_back([&, l, b0, b1] {
+}
+
+static void worker_main(xfg_ctx* c, int l) {
+    (void)hipSetDevice(c->device);
+    Lane* L = c->lanes[l].get();
+    for (;;) {
+        Unit u;
+        bool skip;
+        {
+            std::unique_lock<std::mutex> g(c->qm);
+            std::deque<Unit>::iterator it;
+            auto pick = [&] {
+                for (it = c->q.begin(); it != c->q.end(); ++it)
+                    if (it->lane < 0 || it->lane == l) return true;
+                return false;
+            };
+            c->qcv.wait(g, [&] { return c->stop || pick(); });
+            if (c->stop) return;
+            u = *it;
+            c->q.erase(it);
+            skip = (bool)u.b->err;  // a failed batch drops its remaining units
+            L->timing = c->timing;
+        }
+        Batch* b = u.b;
+        std::exception_ptr e;
+        if (!skip) {
             try {
-                HIPCHK(hipSetDevice(c->device));
-                prove_lane(c->lanes[l].get(), T, ce_div, jobs.data() + b0, b1 - b0, nullptr, n, o);
+                prove_lane(L, b->T, b->ce_div, b->jobs.data() + u.b0, u.b1 - u.b0, b->trace_host, b->n, b->o);
+                copy_unit(b, u.b0, u.b1);
             } catch (...) {
-                errs[l] = std::current_exception();
+                e = std::current_exception();
             }
-        });
+        }
+        std::lock_guard<std::mutex> g(c->qm);
+        if (e && !b->err) b->err = e;
+        c->last_lane = l;
+        if (--b->units_left == 0) c->dcv.notify_all();
     }
-    for (auto& t : th) t.join();
-    for (auto& e : errs)
-        if (e) std::rethrow_exception(e);
+}
+
+static void ensure_workers(xfg_ctx* c) {
+    const int nl = max_lanes();
+    ensure_lanes(c, nl);
+    while ((int)c->workers.size() < nl) {
+        int l = (int)c->workers.size();
+        c->workers.emplace_back(worker_main, c, l);
+    }
+}
+
+// blocks until no submitted unit is queued or running (tables may only be replaced then)
+static void drain(xfg_ctx* c) {
+    std::unique_lock<std::mutex> g(c->qm);
+    c->dcv.wait(g, [&] {
+        for (auto& kv : c->pending)
+            if (kv.second->units_left) return false;
+        return true;
+    });
+}
+
+static void bind_tables(xfg_ctx* c, Batch* b) {
+    const int LM = (int)(ilog2(b->n) + ilog2(b->o.beta));
+    if (c->tables.LM < LM) {
+        drain(c);
+        ensure_tables(c, LM);
+    }
+    b->T = tables_of(c);
+    b->ce_div = ensure_ce_table(c, (int)ilog2(b->n));
+}
+
+// units of unit_size() proofs (the whole batch as one unit in timing mode, so the per-stage
+// times describe one launch set of the batch)
+static std::vector<Unit> split_units(xfg_ctx* c, int B) {
+    std::vector<Unit> u;
+    const int U = c->timing ? std::max(1, B) : unit_size();
+    for (int b0 = 0; b0 < B; b0 += U) u.push_back(Unit{nullptr, b0, std::min(B, b0 + U), -1});
+    return u;
+}
+
+static uint64_t enqueue(xfg_ctx* c, std::unique_ptr<Batch> bp, std::vector<Unit> units) {
+    ensure_workers(c);
+    Batch* b = bp.get();
+    b->st.assign(b->jobs.size(), XFG_OK);
+    std::lock_guard<std::mutex> g(c->qm);
+    uint64_t t = c->next_ticket++;
+    b->units_left = (int)units.size();
+    c->pending[t] = std::move(bp);
+    for (auto& u : units) {
+        u.b = b;
+        c->q.push_back(u);
+    }
+    c->qcv.notify_all();
+    return t;
+}
+
+static std::unique_ptr<Batch> wait_batch(xfg_ctx* c, uint64_t t) {
+    std::unique_lock<std::mutex> g(c->qm);
+    auto it = c->pending.find(t);
+    if (it == c->pending.end()) return nullptr;
+    Batch* b = it->second.get();
+    c->dcv.wait(g, [&] { return b->units_left == 0; });
+    std::unique_ptr<Batch> bp = std::move(it->second);
+    c->pending.erase(it);
+    return bp;
+}
+
+static bool busy(xfg_ctx* c) {
+    std::lock_guard<std::mutex> g(c->qm);
+    return !c->pending.empty();
 }
 
 static int copy_out(xfg_ctx* c, const std::vector<uint8_t>& bytes, uint8_t* out, size_t* out_len) {
@@ -1046,6 +1243,13 @@ xfg_ctx* xfg_ctx_create(int device_id) {
 
 void xfg_ctx_destroy(xfg_ctx* c) {
     if (!c) return;
+    drain(c);
+    {
+        std::lock_guard<std::mutex> g(c->qm);
+        c->stop = true;
+        c->qcv.notify_all();
+    }
+    for (auto& t : c->workers) t.join();
     (void)hipSetDevice(c->device);
     for (auto& L : c->lanes) {
         (void)hipStreamSynchronize(L->stream);
@@ -1056,7 +1260,7 @@ void xfg_ctx_destroy(xfg_ctx* c) {
     c->tables.tw.release();
     c->tables.pow7.release();
     c->tables.ipow7.release();
-    c->tables.ce_div.release();
+    for (auto& kv : c->tables.ce_div) kv.second.release();
     delete c;
 }
 
@@ -1124,28 +1328,41 @@ int xfg_prove_trace(xfg_ctx* c, const uint64_t* trace, uint32_t width, uint64_t 
         }
     return guarded(c, [&]() -> int {
         HIPCHK(hipSetDevice(c->device));
-        std::vector<ProofJob> jobs(1);
-        memset(&jobs[0].air, 0, sizeof(AirConst));
-        memcpy(jobs[0].air.pub, air->pub_inputs, sizeof air->pub_inputs);
-        jobs[0].air.nullifier = air->nullifier;
-        jobs[0].air.commitment = air->commitment;
-        prove_jobs(c, jobs, trace, n, o);
-        if (jobs[0].status) {
+        std::unique_ptr<Batch> bp(new Batch());
+        bp->jobs.resize(1);
+        ProofJob& j = bp->jobs[0];
+        memset(&j.air, 0, sizeof(AirConst));
+        memcpy(j.air.pub, air->pub_inputs, sizeof air->pub_inputs);
+        j.air.nullifier = air->nullifier;
+        j.air.commitment = air->commitment;
+        bp->which = {0};
+        bp->outs = {out};
+        bp->out_lens = out_len;
+        bp->trace_host = trace;
+        bp->n = n;
+        bp->o = o;
+        bind_tables(c, bp.get());
+        std::unique_ptr<Batch> b = wait_batch(c, enqueue(c, std::move(bp), {Unit{nullptr, 0, 1, -1}}));
+        if (b->err) std::rethrow_exception(b->err);
+        if (b->st[0] == XFG_PROVER_ERROR) {
             c->err = "Prover error: proof generation failed (degenerate transcript or DEEP degree)";
-            return jobs[0].status;
+        } else if (b->st[0] == XFG_BUFFER_TOO_SMALL) {
+            c->err = "output buffer too small";
         }
-        return copy_out(c, jobs[0].bytes, out, out_len);
+        return b->st[0];
     });
 }
 
-int xfg_prove_batch(xfg_ctx* c, uint32_t count, const xfg_burn_inputs* inputs, uint64_t trace_length,
-                    const xfg_options* opts, uint8_t* const* outs, size_t* out_lens, int* statuses) {
+int xfg_prove_batch_submit(xfg_ctx* c, uint32_t count, const xfg_burn_inputs* inputs, uint64_t trace_length,
+                           const xfg_options* opts, uint8_t* const* outs, size_t* out_lens, int* statuses,
+                           uint64_t* ticket) {
     if (!c) return XFG_INVALID_ARGUMENT;
     c->err.clear();
-    if (!inputs || !opts || !out_lens || !statuses || count == 0) {
+    if (!inputs || !opts || !out_lens || !statuses || !ticket || count == 0) {
         c->err = "null argument";
         return XFG_INVALID_ARGUMENT;
     }
+    *ticket = 0;
     u64 n = trace_length ? trace_length : 64;
     Opts o = to_opts(opts);
     if (const char* m = check_options(n, o)) {
@@ -1154,8 +1371,7 @@ int xfg_prove_batch(xfg_ctx* c, uint32_t count, const xfg_burn_inputs* inputs, u
     }
     return guarded(c, [&]() -> int {
         HIPCHK(hipSetDevice(c->device));
-        std::vector<ProofJob> jobs;
-        std::vector<uint32_t> which;
+        std::unique_ptr<Batch> bp(new Batch());
         for (uint32_t i = 0; i < count; i++) {
             AirConst a;
             std::string err;
@@ -1165,24 +1381,47 @@ int xfg_prove_batch(xfg_ctx* c, uint32_t count, const xfg_burn_inputs* inputs, u
                 c->err = err;
                 continue;
             }
-            ProofJob j;
-            j.air = a;
-            jobs.push_back(std::move(j));
-            which.push_back(i);
+            bp->jobs.emplace_back();
+            bp->jobs.back().air = a;
+            bp->which.push_back(i);
         }
-        if (!jobs.empty()) prove_jobs(c, jobs, nullptr, n, o);
-        for (size_t k = 0; k < jobs.size(); k++) {
-            uint32_t i = which[k];
-            if (jobs[k].status) {
-                statuses[i] = jobs[k].status;
-                continue;
-            }
-            size_t len = out_lens[i];
-            statuses[i] = copy_out(c, jobs[k].bytes, outs ? outs[i] : nullptr, &len);
-            out_lens[i] = len;
+        if (outs) bp->outs.assign(outs, outs + count);
+        bp->out_lens = out_lens;
+        bp->statuses = statuses;
+        bp->n = n;
+        bp->o = o;
+        bind_tables(c, bp.get());
+        std::vector<Unit> units = split_units(c, (int)bp->jobs.size());
+        *ticket = enqueue(c, std::move(bp), std::move(units));
+        return XFG_OK;
+    });
+}
+
+int xfg_batch_wait(xfg_ctx* c, uint64_t ticket) {
+    if (!c) return XFG_INVALID_ARGUMENT;
+    return guarded(c, [&]() -> int {
+        std::unique_ptr<Batch> b = wait_batch(c, ticket);
+        if (!b) {
+            c->err = "unknown batch ticket";
+            return XFG_INVALID_ARGUMENT;
+        }
+        if (b->err) std::rethrow_exception(b->err);
+        for (size_t k = 0; k < b->jobs.size(); k++) {
+            b->statuses[b->which[k]] = b->st[k];
+            if (b->st[k] == XFG_BUFFER_TOO_SMALL) c->err = "output buffer too small";
+            if (b->st[k] == XFG_PROVER_ERROR)
+                c->err = "Prover error: proof generation failed (degenerate transcript or DEEP degree)";
         }
         return XFG_OK;
     });
+}
+
+int xfg_prove_batch(xfg_ctx* c, uint32_t count, const xfg_burn_inputs* inputs, uint64_t trace_length,
+                    const xfg_options* opts, uint8_t* const* outs, size_t* out_lens, int* statuses) {
+    uint64_t t = 0;
+    int r = xfg_prove_batch_submit(c, count, inputs, trace_length, opts, outs, out_lens, statuses, &t);
+    if (r) return r;
+    return xfg_batch_wait(c, t);
 }
 
 int xfg_prepare(xfg_ctx* c, uint32_t count, uint64_t trace_length, const xfg_options* opts) {
@@ -1212,10 +1451,20 @@ int xfg_prepare(xfg_ctx* c, uint32_t count, uint64_t trace_length, const xfg_opt
         AirConst a;
         std::string err;
         if (marshal(&in, a, err)) return XFG_PROVER_ERROR;
+        // every lane proves one full unit, twice (lane-pinned units)
+        ensure_workers(c);
+        const int nl = (int)c->workers.size(), U = std::min<int>((int)count, unit_size());
         for (int pass = 0; pass < 2; pass++) {
-            std::vector<ProofJob> jobs(count);
-            for (auto& j : jobs) j.air = a;
-            prove_jobs(c, jobs, nullptr, n, o);
+            std::unique_ptr<Batch> bp(new Batch());
+            bp->jobs.resize((size_t)nl * U);
+            for (auto& j : bp->jobs) j.air = a;
+            bp->n = n;
+            bp->o = o;
+            bind_tables(c, bp.get());
+            std::vector<Unit> units;
+            for (int l = 0; l < nl; l++) units.push_back(Unit{nullptr, l * U, (l + 1) * U, l});
+            std::unique_ptr<Batch> b = wait_batch(c, enqueue(c, std::move(bp), std::move(units)));
+            if (b->err) std::rethrow_exception(b->err);
         }
         HIPCHK(hipDeviceSynchronize());
         return XFG_OK;
@@ -1254,7 +1503,7 @@ int xfg_stage_times(const xfg_ctx* c, double* ms, const char** names, int max) {
     if (!c) return 0;
     int k = std::min<int>(max, ST_COUNT);
     for (int i = 0; i < k; i++) {
-        if (ms) ms[i] = c->lanes.empty() ? 0.0 : c->lanes[0]->stage_ms[i];
+        if (ms) ms[i] = c->lanes.empty() ? 0.0 : c->lanes[c->last_lane]->stage_ms[i];
         if (names) names[i] = STAGE_NAMES[i];
     }
     return k;
@@ -1263,6 +1512,10 @@ int xfg_stage_times(const xfg_ctx* c, double* ms, const char** names, int max) {
 int xfg_bench_lde(xfg_ctx* c, uint32_t count, uint64_t n, uint32_t blowup, uint32_t iters, double* avg_ms) {
     if (!c || !avg_ms || !is_pow2(n) || !is_pow2(blowup) || n < 8 || blowup < 2 || blowup > 16 || iters == 0)
         return XFG_INVALID_ARGUMENT;
+    if (busy(c)) {  // lane 0's stream and buffers belong to the workers while batches are pending
+        c->err = "batches pending: call xfg_batch_wait first";
+        return XFG_INVALID_ARGUMENT;
+    }
     return guarded(c, [&]() -> int {
         Lane* L = lane0(c);
         HIPCHK(hipSetDevice(c->device));
@@ -1300,6 +1553,10 @@ int xfg_bench_lde(xfg_ctx* c, uint32_t count, uint64_t n, uint32_t blowup, uint3
 int xfg_debug_lde(xfg_ctx* c, const uint64_t* coef, uint32_t npoly, uint64_t n, uint32_t blowup, uint64_t* out) {
     if (!c || !coef || !out || !is_pow2(n) || !is_pow2(blowup) || n < 8 || blowup < 2 || blowup > 16)
         return XFG_INVALID_ARGUMENT;
+    if (busy(c)) {  // lane 0's stream and buffers belong to the workers while batches are pending
+        c->err = "batches pending: call xfg_batch_wait first";
+        return XFG_INVALID_ARGUMENT;
+    }
     return guarded(c, [&]() -> int {
         Lane* L = lane0(c);
         HIPCHK(hipSetDevice(c->device));
@@ -1324,6 +1581,10 @@ int xfg_debug_lde(xfg_ctx* c, const uint64_t* coef, uint32_t npoly, uint64_t n, 
 
 int xfg_debug_interpolate(xfg_ctx* c, const uint64_t* evals, uint32_t npoly, uint64_t n, int offset7, uint64_t* out) {
     if (!c || !evals || !out || !is_pow2(n) || n < 8) return XFG_INVALID_ARGUMENT;
+    if (busy(c)) {  // lane 0's stream and buffers belong to the workers while batches are pending
+        c->err = "batches pending: call xfg_batch_wait first";
+        return XFG_INVALID_ARGUMENT;
+    }
     return guarded(c, [&]() -> int {
         Lane* L = lane0(c);
         HIPCHK(hipSetDevice(c->device));

@@ -56,6 +56,10 @@ _lib.xfg_prove_trace.argtypes = [C.c_void_p, _u64p, C.c_uint32, C.c_uint64, C.PO
                                  C.POINTER(_Options), _u8p, C.POINTER(C.c_size_t)]
 _lib.xfg_prove_batch.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(_BurnInputs), C.c_uint64, C.POINTER(_Options),
                                  C.POINTER(_u8p), C.POINTER(C.c_size_t), C.POINTER(C.c_int)]
+_lib.xfg_prove_batch_submit.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(_BurnInputs), C.c_uint64,
+                                         C.POINTER(_Options), C.POINTER(_u8p), C.POINTER(C.c_size_t),
+                                         C.POINTER(C.c_int), C.POINTER(C.c_uint64)]
+_lib.xfg_batch_wait.argtypes = [C.c_void_p, C.c_uint64]
 _lib.xfg_prepare.argtypes = [C.c_void_p, C.c_uint32, C.c_uint64, C.POINTER(_Options)]
 _lib.xfg_burn_air_consts.argtypes = [C.POINTER(_BurnInputs), C.POINTER(_AirConsts)]
 _lib.xfg_set_timing.argtypes = [C.c_void_p, C.c_int]
@@ -165,6 +169,36 @@ def exported_symbols():
     return [name for name in dir(_lib)]
 
 
+class PendingBatch:
+    """a submitted batch (XfgBurnMintProver.submit_batch); result() -> list of StarkProof | XfgStarkError"""
+
+    def __init__(self, prover, ticket, buf, base, cap, outs, lens, sts):
+        self._p, self._t, self._buf, self._base, self._cap = prover, ticket, buf, base, cap
+        self._outs, self._lens, self._sts = outs, lens, sts
+        self._res = None
+
+    def result(self):
+        if self._res is None:
+            st = _lib.xfg_batch_wait(self._p._ctx, self._t)
+            if st:
+                self._p._free.append(self._buf)
+                raise self._p._err(st)
+            res = []
+            for i in range(len(self._sts)):
+                if self._sts[i]:
+                    res.append(XfgStarkError(self._sts[i], STATUS.get(self._sts[i])))
+                else:
+                    res.append(StarkProof(C.string_at(self._base + i * self._cap, self._lens[i])))
+            self._p._free.append(self._buf)
+            self._res = res
+        return self._res
+
+    def __del__(self):
+        # the workers write into this batch's buffers: never release them before the batch is done
+        if self._res is None and getattr(self._p, "_ctx", None):
+            _lib.xfg_batch_wait(self._p._ctx, self._t)
+
+
 class XfgBurnMintProver:
     """reference XfgBurnMintProver (src/burn_mint_prover.rs:18-244) on one MI355X device."""
 
@@ -239,6 +273,12 @@ class XfgBurnMintProver:
 
     def prove_batch(self, inputs, trace_length=64):
         """list of dicts of prove_burn_mint kwargs -> list of StarkProof | XfgStarkError (per proof)."""
+        return self.submit_batch(inputs, trace_length).result()
+
+    def submit_batch(self, inputs, trace_length=64):
+        """asynchronous prove_batch (xfg_prove_batch_submit): inputs are validated and marshalled
+        now, proving runs on the context's lane workers; PendingBatch.result() waits. Submitting
+        the next batch before collecting this one overlaps their host and device work."""
         k = len(inputs)
         arr = (_BurnInputs * k)()
         keep = []
@@ -248,23 +288,26 @@ class XfgBurnMintProver:
             arr[i] = s
         o = self._options._c()
         cap = _lib.xfg_proof_size_bound(trace_length, C.byref(o))
-        if getattr(self, "_out_cap", 0) < cap * k:
-            self._out = C.create_string_buffer(cap * k)
-            self._out_cap = cap * k
-        base = C.addressof(self._out)
+        buf = self._take_buffer(cap * k)
+        base = C.addressof(buf)
         outs = (_u8p * k)(*[C.cast(base + i * cap, _u8p) for i in range(k)])
         lens = (C.c_size_t * k)(*([cap] * k))
         sts = (C.c_int * k)()
-        st = _lib.xfg_prove_batch(self._ctx, k, arr, trace_length, C.byref(o), outs, lens, sts)
+        ticket = C.c_uint64(0)
+        st = _lib.xfg_prove_batch_submit(self._ctx, k, arr, trace_length, C.byref(o), outs, lens, sts,
+                                         C.byref(ticket))
         if st:
+            self._free.append(buf)
             raise self._err(st)
-        res = []
-        for i in range(k):
-            if sts[i]:
-                res.append(XfgStarkError(sts[i], STATUS.get(sts[i])))
-            else:
-                res.append(StarkProof(C.string_at(base + i * cap, lens[i])))
-        return res
+        return PendingBatch(self, ticket.value, buf, base, cap, outs, lens, sts)
+
+    def _take_buffer(self, size):
+        # output buffers are recycled (a fresh create_string_buffer zero-fills megabytes per batch)
+        free = self.__dict__.setdefault("_free", [])
+        for i, b in enumerate(free):
+            if C.sizeof(b) >= size:
+                return free.pop(i)
+        return C.create_string_buffer(size)
 
     def prepare(self, count, trace_length=64):
         """allocate workspaces for batches of `count` proofs of this shape (setup, untimed)"""
