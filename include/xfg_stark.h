@@ -131,6 +131,12 @@ int xfg_bench_lde(xfg_ctx* ctx, uint32_t count, uint64_t n, uint32_t blowup, uin
 int xfg_debug_lde(xfg_ctx* ctx, const uint64_t* coef, uint32_t npoly, uint64_t n, uint32_t blowup, uint64_t* out);
 int xfg_debug_interpolate(xfg_ctx* ctx, const uint64_t* evals, uint32_t npoly, uint64_t n, int offset7,
                           uint64_t* out);
+/* OOD evaluation + DEEP quotient kernels of the prover on `count` instances: coef [count][7][n],
+ * hcoef [count][n] (trace / composition coefficients), zpts [count][2] = (z, z g), coeffs
+ * [count][8] = 7 trace DEEP coefficients + the composition one; ood_out [count][15] (T_c(z),
+ * T_c(zg) interleaved, H(z)), deep_out [count][n] (DEEP composition coefficients) */
+int xfg_debug_ood_deep(xfg_ctx* ctx, uint32_t count, uint64_t n, const uint64_t* coef, const uint64_t* hcoef,
+                       const uint64_t* zpts, const uint64_t* coeffs, uint64_t* ood_out, uint64_t* deep_out);
 
 #ifdef __cplusplus
 }

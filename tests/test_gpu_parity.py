@@ -64,6 +64,49 @@ def test_interpolate_kernel_matches_oracle(prover, n, off7):
         assert [int(v) for v in got[p]] == want
 
 
+def _ood_deep_reference(co, h, z, zg, a, gam):
+    """T_c(z), T_c(zg), H(z) and the DEEP quotient coefficients (synthetic division), plain ints"""
+    n = len(h)
+
+    def ev(poly, x):
+        acc = 0
+        for v in reversed(poly):
+            acc = (acc * x + v) % P
+        return acc
+    ood = []
+    for c in range(7):
+        ood += [ev(co[c], z), ev(co[c], zg)]
+    ood.append(ev(h, z))
+    c1 = (sum(a[c] * ood[2 * c] for c in range(7)) + gam * ood[14]) % P
+    c2 = sum(a[c] * ood[2 * c + 1] for c in range(7)) % P
+    s = [sum(a[c] * co[c][j] for c in range(7)) % P for j in range(n)]
+    p1 = [(s[j] + gam * h[j]) % P for j in range(n)]
+    p1[0] = (p1[0] - c1) % P
+    p2 = list(s)
+    p2[0] = (p2[0] - c2) % P
+    q1, q2, d = 0, 0, [0] * n
+    for k in range(n - 2, -1, -1):
+        q1 = (p1[k + 1] + z * q1) % P
+        q2 = (p2[k + 1] + zg * q2) % P
+        d[k] = (q1 + q2) % P
+    return ood, d
+
+
+@pytest.mark.parametrize("n,count", [(8, 2), (64, 3), (4096, 2), (1 << 14, 1)])
+def test_ood_deep_kernels_match_reference(prover, n, count):
+    rng = random.Random(n * 31 + count)
+    co = [[[rng.randrange(P) for _ in range(n)] for _ in range(7)] for _ in range(count)]
+    h = [[rng.randrange(P) for _ in range(n)] for _ in range(count)]
+    zp = [[rng.randrange(1, P), rng.randrange(1, P)] for _ in range(count)]
+    cf = [[rng.randrange(P) for _ in range(8)] for _ in range(count)]
+    ood, deep = prover.debug_ood_deep(np.array(co, dtype=np.uint64), np.array(h, dtype=np.uint64),
+                                      np.array(zp, dtype=np.uint64), np.array(cf, dtype=np.uint64))
+    for b in range(count):
+        want_ood, want_deep = _ood_deep_reference(co[b], h[b], zp[b][0], zp[b][1], cf[b][:7], cf[b][7])
+        assert [int(v) for v in ood[b]] == want_ood
+        assert [int(v) for v in deep[b]] == want_deep
+
+
 @pytest.mark.parametrize("src,n,blowup", [("package", 64, 8), ("package", 64, 4), (0, 8, 8), (1, 16, 4), (7, 32, 2),
                                           (2, 128, 8), (3, 1024, 4), (4, 1024, 8), (5, 2048, 16), (6, 4096, 8)])
 def test_prove_trace_bytes_match_oracle(prover, src, n, blowup):

@@ -11,6 +11,7 @@
 //   - FriProver::build_layers: fold-by-8 (apply_drp) and per-layer commitments
 // All arithmetic is 64-bit Goldilocks integer work: HBM/VALU bound, no MFMA.
 #include "kernels.hpp"
+#include <algorithm>
 
 namespace xfg {
 
@@ -318,46 +319,70 @@ void launch_constraint_eval(const u64* lde, const AirConst* air, const u64* coef
 }
 
 // ============================================================================ OOD
-// partial sums of T_c(z), T_c(zg) (c < 7) and H(z); 8 consecutive coefficients per thread
-__global__ __launch_bounds__(256) void ood_partial_kernel(const u64* coef, const u64* hcoef, const u64* zpts,
-                                                          u64* partial, int logn) {
-    __shared__ u64 red[15][256];
+// Blocks own CHUNK = T * OOD_R consecutive coefficients (T = min(256, n / OOD_R) threads, thread t
+// takes j = base + r T + t: coalesced). Per block the 15 partial sums
+//   sum_{j in block} T_c[j] z^j, sum T_c[j] (zg)^j (c < 7), sum H[j] z^j
+// are stored in `partial` [proof][block][15]: ood_final adds them up, and the DEEP quotient reuses
+// them as its per-block carries (no second pass over the coefficients for the block sums).
+#define OOD_R 8
+static inline int ood_threads(u64 n) { return (int)std::min<u64>(256, n / OOD_R); }
+
+__device__ __forceinline__ u64 shfl_xor_u64(u64 v, int m, int w) {
+    u32 lo = __shfl_xor((u32)v, m, w), hi = __shfl_xor((u32)(v >> 32), m, w);
+    return (u64)lo | ((u64)hi << 32);
+}
+
+__global__ __launch_bounds__(256) void ood_kernel(const u64* coef, const u64* hcoef, const u64* zpts, u64* partial,
+                                                  int logn) {
+    __shared__ u64 zb[4];
+    __shared__ u64 red[4][15];
     const u64 n = 1ULL << logn;
-    const int proof = blockIdx.y, tid = threadIdx.x;
-    const u64 j0 = ((u64)blockIdx.x * blockDim.x + tid) * 8;
+    const int proof = blockIdx.y, t = threadIdx.x, T = blockDim.x;
+    const u64 base = (u64)blockIdx.x * T * OOD_R;
     const u64 z = zpts[2 * proof], zg = zpts[2 * proof + 1];
+    if (t == 0) {
+        zb[0] = gl_pow(z, base);
+        zb[1] = gl_pow(zg, base);
+        zb[2] = gl_pow(z, (u64)T);
+        zb[3] = gl_pow(zg, (u64)T);
+    }
+    __syncthreads();
+    u64 pz = gl_mul(zb[0], gl_pow(z, (u64)t)), pzg = gl_mul(zb[1], gl_pow(zg, (u64)t));
+    const u64 zT = zb[2], zgT = zb[3];
+    const u64* co = coef + (u64)proof * 7 * n;
+    const u64* h = hcoef + (u64)proof * n;
     u64 acc[15];
 #pragma unroll
     for (int q = 0; q < 15; q++) acc[q] = 0;
-    if (j0 < n) {
-        u64 pz = gl_pow(z, j0), pzg = gl_pow(zg, j0);
-        const u64* co = coef + (u64)proof * 7 * n;
-        const u64* h = hcoef + (u64)proof * n;
-        const int cnt = n - j0 < 8 ? (int)(n - j0) : 8;
-        for (int r = 0; r < cnt; r++) {
-            u64 j = j0 + r;
+#pragma unroll 2
+    for (int r = 0; r < OOD_R; r++) {
+        const u64 j = base + (u64)r * T + t;
 #pragma unroll
-            for (int c = 0; c < 7; c++) {
-                u64 v = co[(u64)c * n + j];
-                acc[2 * c] = gl_add(acc[2 * c], gl_mul(v, pz));
-                acc[2 * c + 1] = gl_add(acc[2 * c + 1], gl_mul(v, pzg));
-            }
-            acc[14] = gl_add(acc[14], gl_mul(h[j], pz));
-            pz = gl_mul(pz, z);
-            pzg = gl_mul(pzg, zg);
+        for (int c = 0; c < 7; c++) {
+            u64 v = co[(u64)c * n + j];
+            acc[2 * c] = gl_add(acc[2 * c], gl_mul(v, pz));
+            acc[2 * c + 1] = gl_add(acc[2 * c + 1], gl_mul(v, pzg));
         }
+        acc[14] = gl_add(acc[14], gl_mul(h[j], pz));
+        pz = gl_mul(pz, zT);
+        pzg = gl_mul(pzg, zgT);
     }
+    // wave reduction, then across the (up to 4) waves
+    const int W = T < 64 ? T : 64;
+    for (int m = W / 2; m > 0; m >>= 1) {
 #pragma unroll
-    for (int q = 0; q < 15; q++) red[q][tid] = acc[q];
+        for (int q = 0; q < 15; q++) acc[q] = gl_add(acc[q], shfl_xor_u64(acc[q], m, W));
+    }
+    if ((t & 63) == 0) {
+#pragma unroll
+        for (int q = 0; q < 15; q++) red[t >> 6][q] = acc[q];
+    }
     __syncthreads();
-    for (int off = blockDim.x / 2; off > 0; off >>= 1) {
-        if (tid < off) {
-#pragma unroll
-            for (int q = 0; q < 15; q++) red[q][tid] = gl_add(red[q][tid], red[q][tid + off]);
-        }
-        __syncthreads();
+    for (int q = t; q < 15; q += T) {  // T may be below 15 for short traces
+        u64 v = red[0][q];
+        for (int w = 1; w < (T + 63) / 64; w++) v = gl_add(v, red[w][q]);
+        partial[((u64)proof * gridDim.x + blockIdx.x) * 15 + q] = v;
     }
-    for (int q = tid; q < 15; q += blockDim.x) partial[((u64)proof * gridDim.x + blockIdx.x) * 15 + q] = red[q][0];
 }
 __global__ void ood_final_kernel(const u64* partial, int nblk, u64* ood) {
     const int proof = blockIdx.x, q = threadIdx.x;
@@ -368,149 +393,145 @@ __global__ void ood_final_kernel(const u64* partial, int nblk, u64* ood) {
 }
 void launch_ood(const u64* coef, const u64* hcoef, const u64* zpts, u64* partial, u64* ood, int logn, int npoly,
                 hipStream_t s) {
-    u64 n = 1ULL << logn;
-    u64 nthreads = (n + 7) / 8;
-    int threads = nthreads < 256 ? (int)nthreads : 256;
-    int nblk = (int)((nthreads + threads - 1) / threads);
-    hipLaunchKernelGGL(ood_partial_kernel, dim3(nblk, npoly), dim3(threads), 0, s, coef, hcoef, zpts, partial, logn);
+    const u64 n = 1ULL << logn;
+    const int T = ood_threads(n), nblk = (int)(n / ((u64)T * OOD_R));
+    hipLaunchKernelGGL(ood_kernel, dim3(nblk, npoly), dim3(T), 0, s, coef, hcoef, zpts, partial, logn);
     hipLaunchKernelGGL(ood_final_kernel, dim3(npoly), dim3(64), 0, s, partial, nblk, ood);
     XFG_CHECK_LAUNCH();
 }
+u64 ood_partial_count(int logn) {
+    const u64 n = 1ULL << logn;
+    return n / ((u64)ood_threads(n) * OOD_R);
+}
 
 // ============================================================================ DEEP
-// P1_j = sum a_c T_c[j] + gamma H[j] - [j==0] c1 ; P2_j = sum a_c T_c[j] - [j==0] c2
-// quotient of P/(x - b): q_k = sum_{j>k} P_j b^(j-k-1) = b^-(k+1) * sum_{j>k} P_j b^j
-// s_j = P_j b^j (two streams) -> exclusive suffix sums -> d_k = z^-(k+1) E1_k + zg^-(k+1) E2_k
-#define DEEP_PER_THREAD 8
-__device__ __forceinline__ void deep_terms(const u64* co, const u64* h, const DeepParams& P, u64 n, u64 j, u64& p1,
-                                           u64& p2) {
-    u64 s = 0;
-#pragma unroll
-    for (int c = 0; c < 7; c++) s = gl_add(s, gl_mul(P.a[c], co[(u64)c * n + j]));
-    p1 = gl_add(s, gl_mul(P.gamma, h[j]));
-    p2 = s;
-    if (j == 0) {
-        p1 = gl_sub(p1, P.c1);
-        p2 = gl_sub(p2, P.c2);
-    }
-}
-__global__ __launch_bounds__(256) void deep_blocksum_kernel(const u64* coef, const u64* hcoef, const DeepParams* dp,
-                                                            u64* bsum, int logn) {
-    __shared__ u64 r1[256], r2[256];
-    const u64 n = 1ULL << logn;
-    const int proof = blockIdx.y, tid = threadIdx.x;
+// DEEP quotient in coefficient form: P1_j = sum a_c T_c[j] + gamma H[j] - [j==0] c1,
+// P2_j = sum a_c T_c[j] - [j==0] c2; d_k = q1_k + q2_k with the synthetic-division recurrences
+//   q1_k = P1_{k+1} + z q1_{k+1},  q2_k = P2_{k+1} + zg q2_{k+1},  q_{n-1} = 0.
+// Same block chunking as the OOD kernel. Block b's entry carry q_e (e = last index of the block)
+// is z^-(e+1) * sum_{j > e} P_j z^j, a weighted suffix sum of the OOD block partials
+// (deep_carry_kernel). Inside a block every thread owns OOD_R consecutive indices: a backward
+// Horner pass gives its chunk map Q_out = L + z^R Q_in, a suffix scan over threads with the
+// uniform multiplier z^R gives each thread's Q_in, and a second backward pass writes d_k.
+__global__ void deep_carry_kernel(const u64* partial, const DeepParams* dp, u64* carry, int nblk, int logch,
+                                  int nproof) {
+    const int proof = blockIdx.x * blockDim.x + threadIdx.x;
+    if (proof >= nproof) return;
     const DeepParams P = dp[proof];
-    const u64* co = coef + (u64)proof * 7 * n;
-    const u64* h = hcoef + (u64)proof * n;
-    const u64 j0 = ((u64)blockIdx.x * blockDim.x + tid) * DEEP_PER_THREAD;
-    u64 s1 = 0, s2 = 0;
-    if (j0 < n) {
-        u64 pz = gl_pow(P.z, j0), pzg = gl_pow(P.zg, j0);
-        for (int r = 0; r < DEEP_PER_THREAD && j0 + r < n; r++) {
-            u64 p1, p2;
-            deep_terms(co, h, P, n, j0 + r, p1, p2);
-            s1 = gl_add(s1, gl_mul(p1, pz));
-            s2 = gl_add(s2, gl_mul(p2, pzg));
-            pz = gl_mul(pz, P.z);
-            pzg = gl_mul(pzg, P.zg);
-        }
-    }
-    r1[tid] = s1;
-    r2[tid] = s2;
-    __syncthreads();
-    for (int off = blockDim.x / 2; off > 0; off >>= 1) {
-        if (tid < off) {
-            r1[tid] = gl_add(r1[tid], r1[tid + off]);
-            r2[tid] = gl_add(r2[tid], r2[tid + off]);
-        }
-        __syncthreads();
-    }
-    if (tid == 0) {
-        bsum[((u64)proof * gridDim.x + blockIdx.x) * 2] = r1[0];
-        bsum[((u64)proof * gridDim.x + blockIdx.x) * 2 + 1] = r2[0];
-    }
-}
-// exclusive suffix sums over blocks (serial per proof; nblk is small)
-__global__ void deep_carry_kernel(const u64* bsum, u64* carry, int nblk) {
-    const int proof = blockIdx.x, q = threadIdx.x;
-    if (q >= 2) return;
-    u64 s = 0;
+    const u64 CH = 1ULL << logch;
+    const u64 zc = gl_pow(P.z, CH), zgc = gl_pow(P.zg, CH);
+    u64 wz = gl_pow(gl_pow(P.zinv, CH), (u64)nblk), wzg = gl_pow(gl_pow(P.zginv, CH), (u64)nblk);
+    u64 S1 = 0, S2 = 0;
     for (int b = nblk - 1; b >= 0; b--) {
-        carry[((u64)proof * nblk + b) * 2 + q] = s;
-        s = gl_add(s, bsum[((u64)proof * nblk + b) * 2 + q]);
+        carry[((u64)proof * nblk + b) * 2] = gl_mul(S1, wz);  // wz = z^-((b+1) CH)
+        carry[((u64)proof * nblk + b) * 2 + 1] = gl_mul(S2, wzg);
+        const u64* pp = partial + ((u64)proof * nblk + b) * 15;
+        u64 t1 = 0, t2 = 0;
+        for (int c = 0; c < 7; c++) {
+            t1 = gl_add(t1, gl_mul(P.a[c], pp[2 * c]));
+            t2 = gl_add(t2, gl_mul(P.a[c], pp[2 * c + 1]));
+        }
+        u64 b1 = gl_add(t1, gl_mul(P.gamma, pp[14])), b2 = t2;
+        if (b == 0) {
+            b1 = gl_sub(b1, P.c1);
+            b2 = gl_sub(b2, P.c2);
+        }
+        S1 = gl_add(S1, b1);
+        S2 = gl_add(S2, b2);
+        wz = gl_mul(wz, zc);
+        wzg = gl_mul(wzg, zgc);
     }
 }
+__device__ __forceinline__ int dpad(int i) { return i + i / OOD_R; }  // chunk stride R+1: no bank pile-up
 __global__ __launch_bounds__(256) void deep_final_kernel(const u64* coef, const u64* hcoef, const DeepParams* dp,
                                                          const u64* carry, u64* deep, int logn) {
-    __shared__ u64 e1[256], e2[256];
+    constexpr int R = OOD_R, CHMAX = 256 * OOD_R;
+    __shared__ u64 s1[CHMAX + CHMAX / R], s2[CHMAX + CHMAX / R];
+    __shared__ u64 S1[256], S2[256];
     const u64 n = 1ULL << logn;
-    const int proof = blockIdx.y, tid = threadIdx.x, T = blockDim.x;
+    const int proof = blockIdx.y, t = threadIdx.x, T = blockDim.x;
+    const u64 base = (u64)blockIdx.x * T * R;
     const DeepParams P = dp[proof];
     const u64* co = coef + (u64)proof * 7 * n;
     const u64* h = hcoef + (u64)proof * n;
-    const u64 j0 = ((u64)blockIdx.x * T + tid) * DEEP_PER_THREAD;
-    u64 s1[DEEP_PER_THREAD], s2[DEEP_PER_THREAD];
-    u64 t1 = 0, t2 = 0;
-    {
-        u64 pz = j0 < n ? gl_pow(P.z, j0) : 0, pzg = j0 < n ? gl_pow(P.zg, j0) : 0;
+    // 1. P1, P2 (coalesced reads) into LDS
+#pragma unroll 2
+    for (int r = 0; r < R; r++) {
+        const int li = r * T + t;
+        const u64 j = base + li;
+        u64 sacc = 0;
 #pragma unroll
-        for (int r = 0; r < DEEP_PER_THREAD; r++) {
-            s1[r] = s2[r] = 0;
-            if (j0 + r < n) {
-                u64 p1, p2;
-                deep_terms(co, h, P, n, j0 + r, p1, p2);
-                s1[r] = gl_mul(p1, pz);
-                s2[r] = gl_mul(p2, pzg);
-                pz = gl_mul(pz, P.z);
-                pzg = gl_mul(pzg, P.zg);
-            }
-            t1 = gl_add(t1, s1[r]);
-            t2 = gl_add(t2, s2[r]);
+        for (int c = 0; c < 7; c++) sacc = gl_add(sacc, gl_mul(P.a[c], co[(u64)c * n + j]));
+        u64 p1 = gl_add(sacc, gl_mul(P.gamma, h[j])), p2 = sacc;
+        if (j == 0) {
+            p1 = gl_sub(p1, P.c1);
+            p2 = gl_sub(p2, P.c2);
         }
+        s1[dpad(li)] = p1;
+        s2[dpad(li)] = p2;
     }
-    // inclusive suffix scan of per-thread totals
-    e1[tid] = t1;
-    e2[tid] = t2;
+    __syncthreads();
+    // 2. chunk maps: L = sum_i z^i P_{a+i}
+    const int a = t * R;
+    u64 L1 = 0, L2 = 0;
+#pragma unroll
+    for (int i = R - 1; i >= 0; i--) {
+        L1 = gl_add(s1[dpad(a + i)], gl_mul(P.z, L1));
+        L2 = gl_add(s2[dpad(a + i)], gl_mul(P.zg, L2));
+    }
+    // 3. suffix scan over threads, multiplier w = z^R; the block carry enters through the last thread
+    u64 w1 = P.z, w2 = P.zg;
+#pragma unroll
+    for (int i = 1; i < R; i <<= 1) {
+        w1 = gl_mul(w1, w1);
+        w2 = gl_mul(w2, w2);
+    }
+    const u64 cin1 = carry[((u64)proof * gridDim.x + blockIdx.x) * 2];
+    const u64 cin2 = carry[((u64)proof * gridDim.x + blockIdx.x) * 2 + 1];
+    if (t == T - 1) {
+        L1 = gl_add(L1, gl_mul(w1, cin1));
+        L2 = gl_add(L2, gl_mul(w2, cin2));
+    }
+    S1[t] = L1;
+    S2[t] = L2;
     __syncthreads();
     for (int off = 1; off < T; off <<= 1) {
-        u64 a1 = e1[tid], a2 = e2[tid];
-        if (tid + off < T) {
-            a1 = gl_add(a1, e1[tid + off]);
-            a2 = gl_add(a2, e2[tid + off]);
+        u64 v1 = S1[t], v2 = S2[t];
+        if (t + off < T) {
+            v1 = gl_add(v1, gl_mul(w1, S1[t + off]));
+            v2 = gl_add(v2, gl_mul(w2, S2[t + off]));
         }
         __syncthreads();
-        e1[tid] = a1;
-        e2[tid] = a2;
+        S1[t] = v1;
+        S2[t] = v2;
         __syncthreads();
+        w1 = gl_mul(w1, w1);
+        w2 = gl_mul(w2, w2);
     }
-    // exclusive suffix (everything after this thread's chunk) + blocks after this one
-    u64 c1 = carry[((u64)proof * gridDim.x + blockIdx.x) * 2];
-    u64 c2 = carry[((u64)proof * gridDim.x + blockIdx.x) * 2 + 1];
-    u64 x1 = gl_add(c1, tid + 1 < T ? e1[tid + 1] : 0);
-    u64 x2 = gl_add(c2, tid + 1 < T ? e2[tid + 1] : 0);
-    if (j0 >= n) return;
-    // walk the chunk backwards: E_k = sum_{j>k} s_j
-    const int cnt = n - j0 < DEEP_PER_THREAD ? (int)(n - j0) : DEEP_PER_THREAD;
-    u64 last = j0 + cnt - 1;
-    u64 iz = gl_pow(P.zinv, last + 1), izg = gl_pow(P.zginv, last + 1);
-    u64* out = deep + (u64)proof * n;
-    for (int r = cnt - 1; r >= 0; r--) {
-        out[j0 + r] = gl_add(gl_mul(iz, x1), gl_mul(izg, x2));
-        x1 = gl_add(x1, s1[r]);
-        x2 = gl_add(x2, s2[r]);
-        iz = gl_mul(iz, P.z);
-        izg = gl_mul(izg, P.zg);
+    u64 q1 = t + 1 < T ? S1[t + 1] : cin1, q2 = t + 1 < T ? S2[t + 1] : cin2;
+    // 4. backward pass over the chunk: d_k = q1_k + q2_k, then step to k - 1
+#pragma unroll
+    for (int i = R - 1; i >= 0; i--) {
+        const int k = dpad(a + i);
+        const u64 p1 = s1[k], p2 = s2[k];
+        s1[k] = gl_add(q1, q2);
+        q1 = gl_add(p1, gl_mul(P.z, q1));
+        q2 = gl_add(p2, gl_mul(P.zg, q2));
     }
+    __syncthreads();
+    u64* out = deep + (u64)proof * n + base;
+#pragma unroll
+    for (int r = 0; r < R; r++) out[r * T + t] = s1[dpad(r * T + t)];
 }
-void launch_deep(const u64* coef, const u64* hcoef, const DeepParams* dp, u64* bsum, u64* carry, u64* deep, int logn,
-                 int npoly, hipStream_t s) {
-    u64 n = 1ULL << logn;
-    u64 nthreads = (n + DEEP_PER_THREAD - 1) / DEEP_PER_THREAD;
-    int threads = nthreads < 256 ? (int)nthreads : 256;
-    int nblk = (int)((nthreads + threads - 1) / threads);
-    hipLaunchKernelGGL(deep_blocksum_kernel, dim3(nblk, npoly), dim3(threads), 0, s, coef, hcoef, dp, bsum, logn);
-    hipLaunchKernelGGL(deep_carry_kernel, dim3(npoly), dim3(64), 0, s, bsum, carry, nblk);
-    hipLaunchKernelGGL(deep_final_kernel, dim3(nblk, npoly), dim3(threads), 0, s, coef, hcoef, dp, carry, deep, logn);
+void launch_deep(const u64* coef, const u64* hcoef, const DeepParams* dp, const u64* partial, u64* carry, u64* deep,
+                 int logn, int npoly, hipStream_t s) {
+    const u64 n = 1ULL << logn;
+    const int T = ood_threads(n), nblk = (int)(n / ((u64)T * OOD_R));
+    int logch = 0;
+    while ((1ULL << logch) < (u64)T * OOD_R) logch++;
+    hipLaunchKernelGGL(deep_carry_kernel, dim3((npoly + 63) / 64), dim3(64), 0, s, partial, dp, carry, nblk, logch,
+                       npoly);
+    hipLaunchKernelGGL(deep_final_kernel, dim3(nblk, npoly), dim3(T), 0, s, coef, hcoef, dp, carry, deep, logn);
     XFG_CHECK_LAUNCH();
 }
 

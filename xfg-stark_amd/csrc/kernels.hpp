@@ -64,10 +64,13 @@ void launch_constraint_eval(const u64* lde, const AirConst* air, const u64* coef
                             u64* ce, int logn, int logbeta, int npoly, hipStream_t s);
 
 // ---- OOD / DEEP ----
+// partial: [B][ood_partial_count(logn)][15] per-block sums, kept for launch_deep
 void launch_ood(const u64* coef, const u64* hcoef, const u64* zpts /*[B][2]*/, u64* partial, u64* ood /*[B][15]*/,
                 int logn, int npoly, hipStream_t s);
-void launch_deep(const u64* coef, const u64* hcoef, const DeepParams* dp, u64* bsum, u64* carry, u64* deep, int logn,
-                 int npoly, hipStream_t s);
+u64 ood_partial_count(int logn);
+// carry: [B][ood_partial_count(logn)][2]
+void launch_deep(const u64* coef, const u64* hcoef, const DeepParams* dp, const u64* partial, u64* carry, u64* deep,
+                 int logn, int npoly, hipStream_t s);
 
 // ---- FRI ----
 void launch_fri_fold(const u64* vals, u64 val_stride, bool coset_major, int logn, int logbeta, u64 rows, int logD,

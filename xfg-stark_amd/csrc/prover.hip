@@ -389,7 +389,7 @@ struct Lane {
     double stage_ms[ST_COUNT] = {0};
     hipEvent_t ev[ST_COUNT + 1] = {};
     DBuf<AirConst> air;
-    DBuf<u64> coeffs, trace, coef, scratch, lde, ce, hcoef, hlde, zpts, partial, ood, bsum, carry, deep, f0, alpha7,
+    DBuf<u64> coeffs, trace, coef, scratch, lde, ce, hcoef, hlde, zpts, partial, ood, carry, deep, f0, alpha7,
         rem, gidx, gval, dn2;
     DBuf<Digest> tnodes, hnodes, gdig;
     DBuf<DeepParams> dp;
@@ -406,7 +406,7 @@ struct Lane {
         h_air.release();
         h_dp.release();
         air.release();
-        for (auto* b : {&coeffs, &trace, &coef, &scratch, &lde, &ce, &hcoef, &hlde, &zpts, &partial, &ood, &bsum,
+        for (auto* b : {&coeffs, &trace, &coef, &scratch, &lde, &ce, &hcoef, &hlde, &zpts, &partial, &ood,
                         &carry, &deep, &f0, &alpha7, &rem, &gidx, &gval, &dn2})
             b->release();
         for (auto* b : {&tnodes, &hnodes, &gdig}) b->release();
@@ -581,11 +581,10 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     c->hlde.ensure((size_t)B * N);
     c->hnodes.ensure((size_t)B * 2 * n);
     c->zpts.ensure((size_t)B * 2);
-    c->partial.ensure((size_t)B * 15 * (n / 8 / 256 + 2));
+    c->partial.ensure((size_t)B * 15 * ood_partial_count(logn));
     c->ood.ensure((size_t)B * 15);
     c->dp.ensure(B);
-    c->bsum.ensure((size_t)B * 2 * (n / 8 / 256 + 2));
-    c->carry.ensure((size_t)B * 2 * (n / 8 / 256 + 2));
+    c->carry.ensure((size_t)B * 2 * ood_partial_count(logn));
     c->deep.ensure((size_t)B * n);
     c->f0.ensure((size_t)B * N);
     c->alpha7.ensure(B);
@@ -722,7 +721,7 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         P.c2 = c2;
     }
     HIPCHK(hipMemcpyAsync(c->dp.p, dps, B * sizeof(DeepParams), hipMemcpyHostToDevice, s));
-    launch_deep(c->coef.p, c->hcoef.p, c->dp.p, c->bsum.p, c->carry.p, c->deep.p, logn, B, s);
+    launch_deep(c->coef.p, c->hcoef.p, c->dp.p, c->partial.p, c->carry.p, c->deep.p, logn, B, s);
     launch_lde(c->deep.p, n, c->f0.p, c->scratch.p, B, logn, logbeta, T, s);
     // degree check: deg(DEEP) == n - 2  <=>  coefficient n-2 != 0 (coefficient n-1 is 0 by construction)
     HIPCHK(hipMemcpy2DAsync(c->dn2.p, 8, c->deep.p + (n - 2), n * 8, 8, B, hipMemcpyDeviceToDevice, s));
@@ -1598,6 +1597,61 @@ int xfg_debug_interpolate(xfg_ctx* c, const uint64_t* evals, uint32_t npoly, uin
         launch_interpolate(L->trace.p, n, L->coef.p, n, L->scratch.p, npoly, logn, offset7 != 0, n, T, L->stream);
         HIPCHK(hipMemcpyAsync(out, L->coef.p, (size_t)npoly * n * 8, hipMemcpyDeviceToHost, L->stream));
         HIPCHK(hipStreamSynchronize(L->stream));
+        return XFG_OK;
+    });
+}
+
+int xfg_debug_ood_deep(xfg_ctx* c, uint32_t count, uint64_t n, const uint64_t* coef, const uint64_t* hcoef,
+                       const uint64_t* zpts, const uint64_t* coeffs, uint64_t* ood_out, uint64_t* deep_out) {
+    if (!c || !coef || !hcoef || !zpts || !coeffs || !ood_out || !deep_out || !is_pow2(n) || n < 8 || count == 0)
+        return XFG_INVALID_ARGUMENT;
+    if (busy(c)) {
+        c->err = "batches pending: call xfg_batch_wait first";
+        return XFG_INVALID_ARGUMENT;
+    }
+    return guarded(c, [&]() -> int {
+        Lane* L = lane0(c);
+        HIPCHK(hipSetDevice(c->device));
+        const int logn = (int)ilog2(n);
+        const size_t B = count;
+        L->coef.ensure(B * 7 * n);
+        L->hcoef.ensure(B * n);
+        L->zpts.ensure(B * 2);
+        L->partial.ensure(B * 15 * ood_partial_count(logn));
+        L->carry.ensure(B * 2 * ood_partial_count(logn));
+        L->ood.ensure(B * 15);
+        L->deep.ensure(B * n);
+        L->dp.ensure(B);
+        hipStream_t s = L->stream;
+        HIPCHK(hipMemcpyAsync(L->coef.p, coef, B * 7 * n * 8, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(L->hcoef.p, hcoef, B * n * 8, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemcpyAsync(L->zpts.p, zpts, B * 2 * 8, hipMemcpyHostToDevice, s));
+        launch_ood(L->coef.p, L->hcoef.p, L->zpts.p, L->partial.p, L->ood.p, logn, (int)B, s);
+        HIPCHK(hipMemcpyAsync(ood_out, L->ood.p, B * 15 * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        std::vector<DeepParams> dps(B);
+        for (size_t b = 0; b < B; b++) {  // as prove_lane: c1, c2 from the OOD values
+            DeepParams& P = dps[b];
+            memset(&P, 0, sizeof P);
+            memcpy(P.a, coeffs + b * 8, 7 * 8);
+            P.gamma = coeffs[b * 8 + 7];
+            P.z = zpts[2 * b];
+            P.zg = zpts[2 * b + 1];
+            P.zinv = gl_inv(P.z);
+            P.zginv = gl_inv(P.zg);
+            const u64* o = ood_out + b * 15;
+            u64 c1 = gl_mul(P.gamma, o[14]), c2 = 0;
+            for (int k = 0; k < 7; k++) {
+                c1 = gl_add(c1, gl_mul(P.a[k], o[2 * k]));
+                c2 = gl_add(c2, gl_mul(P.a[k], o[2 * k + 1]));
+            }
+            P.c1 = c1;
+            P.c2 = c2;
+        }
+        HIPCHK(hipMemcpyAsync(L->dp.p, dps.data(), B * sizeof(DeepParams), hipMemcpyHostToDevice, s));
+        launch_deep(L->coef.p, L->hcoef.p, L->dp.p, L->partial.p, L->carry.p, L->deep.p, logn, (int)B, s);
+        HIPCHK(hipMemcpyAsync(deep_out, L->deep.p, B * n * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
         return XFG_OK;
     });
 }

@@ -66,6 +66,7 @@ _lib.xfg_set_timing.argtypes = [C.c_void_p, C.c_int]
 _lib.xfg_stage_times.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_char_p), C.c_int]
 _lib.xfg_bench_lde.argtypes = [C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.POINTER(C.c_double)]
 _lib.xfg_debug_lde.argtypes = [C.c_void_p, _u64p, C.c_uint32, C.c_uint64, C.c_uint32, _u64p]
+_lib.xfg_debug_ood_deep.argtypes = [C.c_void_p, C.c_uint32, C.c_uint64, _u64p, _u64p, _u64p, _u64p, _u64p, _u64p]
 _lib.xfg_debug_interpolate.argtypes = [C.c_void_p, _u64p, C.c_uint32, C.c_uint64, C.c_int, _u64p]
 
 
@@ -341,6 +342,22 @@ class XfgBurnMintProver:
         if st:
             raise self._err(st)
         return out
+
+    def debug_ood_deep(self, coef, hcoef, zpts, coeffs):
+        """OOD + DEEP kernels: coef [B,7,n], hcoef [B,n], zpts [B,2], coeffs [B,8] -> (ood [B,15], deep [B,n])"""
+        import numpy as np
+        c = np.ascontiguousarray(coef, dtype=np.uint64)
+        B, _, n = c.shape
+        hc = np.ascontiguousarray(hcoef, dtype=np.uint64)
+        zp = np.ascontiguousarray(zpts, dtype=np.uint64)
+        co = np.ascontiguousarray(coeffs, dtype=np.uint64)
+        ood = np.zeros((B, 15), dtype=np.uint64)
+        deep = np.zeros((B, n), dtype=np.uint64)
+        p = lambda a: a.ctypes.data_as(_u64p)
+        st = _lib.xfg_debug_ood_deep(self._ctx, B, n, p(c), p(hc), p(zp), p(co), p(ood), p(deep))
+        if st:
+            raise self._err(st)
+        return ood, deep
 
     def debug_interpolate(self, evals, n, offset7=False):
         import numpy as np
