@@ -81,18 +81,41 @@ __device__ __forceinline__ Digest2 pair_subtree(const u64* base, u64 n, u64 m) {
     }
 }
 
+// Block-level continuation of a Merkle level: thread t of a block of T (power of two) threads
+// holds the digest of node blockIdx.x * T + t of the level with `count` nodes (heap [count,
+// 2 count)). The block merges its T nodes up log2(T) levels through LDS, storing every parent, so
+// only count / T nodes are left for launch_tree_top.
+// Levels stop once a level has `wmin` nodes per block (lanes of narrower levels would idle).
+__device__ __forceinline__ void block_tree_up(Digest d, Digest* nodes, u64 count, Digest* lds, int wmin) {
+    const int t = threadIdx.x;
+    u64 c = count;
+    for (int w = blockDim.x; w > wmin; w >>= 1) {
+        lds[t] = d;
+        __syncthreads();
+        c >>= 1;
+        if (t < w / 2) {
+            d = b3_merge(lds[2 * t], lds[2 * t + 1]);
+            nodes[c + (u64)blockIdx.x * (w / 2) + t] = d;
+        }
+        __syncthreads();
+    }
+}
+
 // two consecutive LDE rows per thread: 2 * 2^LOGB leaves, subtree top at level LOGB + 1 =
-// heap node n/2 + m/2
+// heap node n/2 + m/2; then log2(blockDim) levels more in LDS
 template <int NC, int LOGB>
 __global__ __launch_bounds__(256) void leaves_lde_kernel(const u64* lde, Digest* nodes_all, u64 node_stride,
-                                                         int logn) {
+                                                         int logn, int wmin) {
+    __shared__ Digest lds[256];
     const u64 n = 1ULL << logn;
     const int proof = blockIdx.y;
-    const u64 m2 = (u64)blockIdx.x * blockDim.x + threadIdx.x;  // row pair
-    if (2 * m2 >= n) return;
+    const u64 m2 = (u64)blockIdx.x * blockDim.x + threadIdx.x;  // row pair (grid covers n/2 exactly)
     const u64* base = lde + (u64)proof * NC * (1 << LOGB) * n;
     Digest2 d = pair_subtree<NC, LOGB, LOGB, 0>(base, n, 2 * m2);
-    nodes_all[(u64)proof * node_stride + n / 2 + m2] = b3_merge(d.a, d.b);
+    Digest top = b3_merge(d.a, d.b);
+    Digest* nodes = nodes_all + (u64)proof * node_stride;
+    nodes[n / 2 + m2] = top;
+    block_tree_up(top, nodes, n / 2, lds, wmin);
 }
 
 // openings: recompute the local subtree heaps of selected rows; entry e = proof << logn | m
@@ -116,13 +139,24 @@ __global__ __launch_bounds__(64) void open_rows_kernel(const u64* lde, const u64
         default: break;                                                                         \
     }
 
-void launch_leaves_lde(const u64* lde, int nc, Digest* nodes, u64 node_stride, int npoly, int logn, int logbeta,
-                       hipStream_t s) {
-    u64 n = 1ULL << logn;
-    dim3 g((unsigned)((n / 2 + 255) / 256), npoly), b(256);
-    if (nc == 7) { XFG_LOGB_DISPATCH(leaves_lde_kernel, 7, logbeta, g, b, 0, s, lde, nodes, node_stride, logn) }
-    else { XFG_LOGB_DISPATCH(leaves_lde_kernel, 1, logbeta, g, b, 0, s, lde, nodes, node_stride, logn) }
+// in-block Merkle levels continue while a level keeps >= XFG_UP_WMIN nodes per block (default 64:
+// full waves only); the narrower levels go to launch_tree_top
+static int up_wmin(u64 T) {
+    static const int v = [] {
+        const char* e = getenv("XFG_UP_WMIN");
+        return e && *e ? std::max(1, atoi(e)) : 64;
+    }();
+    return (int)std::min<u64>(T, (u64)v);
+}
+u64 launch_leaves_lde(const u64* lde, int nc, Digest* nodes, u64 node_stride, int npoly, int logn, int logbeta,
+                      hipStream_t s) {
+    const u64 n = 1ULL << logn, T = std::min<u64>(256, n / 2);
+    const int wmin = up_wmin(T);
+    dim3 g((unsigned)(n / 2 / T), npoly), b((unsigned)T);
+    if (nc == 7) { XFG_LOGB_DISPATCH(leaves_lde_kernel, 7, logbeta, g, b, 0, s, lde, nodes, node_stride, logn, wmin) }
+    else { XFG_LOGB_DISPATCH(leaves_lde_kernel, 1, logbeta, g, b, 0, s, lde, nodes, node_stride, logn, wmin) }
     XFG_CHECK_LAUNCH();
+    return n / 2 / T * wmin;
 }
 void launch_open_rows(const u64* lde, int nc, const u64* entries, u64 count, Digest* out, int logn, int logbeta,
                       hipStream_t s) {
@@ -210,22 +244,29 @@ __device__ __forceinline__ u64 layer_at(const u64* base, bool coset_major, int l
 // FRI layer leaves (hash_values::<H, E, 8> over transpose_slice rows): leaf i = H(values at
 // natural indices i + k*rows, k < 8). All leaves are stored (layers are N/8 and smaller).
 __global__ __launch_bounds__(256) void fri_leaves_kernel(const u64* vals, u64 val_stride, int coset_major, int logn,
-                                                         int logbeta, u64 rows, Digest* nodes_all, u64 node_stride) {
+                                                         int logbeta, u64 rows, Digest* nodes_all, u64 node_stride,
+                                                         int wmin) {
+    __shared__ Digest lds[256];
     const int proof = blockIdx.y;
-    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= rows) return;
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;  // grid covers rows exactly
     const u64* base = vals + (u64)proof * val_stride;
     u64 v[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) v[k] = layer_at(base, coset_major, logn, logbeta, i + (u64)k * rows);
-    nodes_all[(u64)proof * node_stride + rows + i] = b3_hash_elems<8>(v);
+    Digest d = b3_hash_elems<8>(v);
+    Digest* nodes = nodes_all + (u64)proof * node_stride;
+    nodes[rows + i] = d;
+    block_tree_up(d, nodes, rows, lds, wmin);
 }
-void launch_fri_leaves(const u64* vals, u64 val_stride, bool coset_major, int logn, int logbeta, u64 rows,
-                       Digest* nodes, u64 node_stride, int npoly, hipStream_t s) {
-    dim3 g((unsigned)((rows + 255) / 256), npoly);
-    hipLaunchKernelGGL(fri_leaves_kernel, g, dim3(256), 0, s, vals, val_stride, coset_major ? 1 : 0, logn, logbeta,
-                       rows, nodes, node_stride);
+u64 launch_fri_leaves(const u64* vals, u64 val_stride, bool coset_major, int logn, int logbeta, u64 rows,
+                      Digest* nodes, u64 node_stride, int npoly, hipStream_t s) {
+    const u64 T = std::min<u64>(256, rows);
+    const int wmin = up_wmin(T);
+    dim3 g((unsigned)(rows / T), npoly);
+    hipLaunchKernelGGL(fri_leaves_kernel, g, dim3((unsigned)T), 0, s, vals, val_stride, coset_major ? 1 : 0, logn,
+                       logbeta, rows, nodes, node_stride, wmin);
     XFG_CHECK_LAUNCH();
+    return rows / T * wmin;
 }
 
 // ============================================================================ AIR
@@ -413,33 +454,47 @@ u64 ood_partial_count(int logn) {
 // (deep_carry_kernel). Inside a block every thread owns OOD_R consecutive indices: a backward
 // Horner pass gives its chunk map Q_out = L + z^R Q_in, a suffix scan over threads with the
 // uniform multiplier z^R gives each thread's Q_in, and a second backward pass writes d_k.
-__global__ void deep_carry_kernel(const u64* partial, const DeepParams* dp, u64* carry, int nblk, int logch,
-                                  int nproof) {
-    const int proof = blockIdx.x * blockDim.x + threadIdx.x;
-    if (proof >= nproof) return;
+// one block per proof, one thread per OOD block b: block sums, suffix sum over blocks, weights
+__global__ __launch_bounds__(1024) void deep_carry_kernel(const u64* partial, const DeepParams* dp, u64* carry,
+                                                          int nblk, int logch) {
+    __shared__ u64 S1[1024], S2[1024];
+    const int proof = blockIdx.x, b = threadIdx.x;
     const DeepParams P = dp[proof];
-    const u64 CH = 1ULL << logch;
-    const u64 zc = gl_pow(P.z, CH), zgc = gl_pow(P.zg, CH);
-    u64 wz = gl_pow(gl_pow(P.zinv, CH), (u64)nblk), wzg = gl_pow(gl_pow(P.zginv, CH), (u64)nblk);
-    u64 S1 = 0, S2 = 0;
-    for (int b = nblk - 1; b >= 0; b--) {
-        carry[((u64)proof * nblk + b) * 2] = gl_mul(S1, wz);  // wz = z^-((b+1) CH)
-        carry[((u64)proof * nblk + b) * 2 + 1] = gl_mul(S2, wzg);
+    u64 b1 = 0, b2 = 0;
+    if (b < nblk) {
         const u64* pp = partial + ((u64)proof * nblk + b) * 15;
         u64 t1 = 0, t2 = 0;
+#pragma unroll
         for (int c = 0; c < 7; c++) {
             t1 = gl_add(t1, gl_mul(P.a[c], pp[2 * c]));
             t2 = gl_add(t2, gl_mul(P.a[c], pp[2 * c + 1]));
         }
-        u64 b1 = gl_add(t1, gl_mul(P.gamma, pp[14])), b2 = t2;
+        b1 = gl_add(t1, gl_mul(P.gamma, pp[14]));
+        b2 = t2;
         if (b == 0) {
             b1 = gl_sub(b1, P.c1);
             b2 = gl_sub(b2, P.c2);
         }
-        S1 = gl_add(S1, b1);
-        S2 = gl_add(S2, b2);
-        wz = gl_mul(wz, zc);
-        wzg = gl_mul(wzg, zgc);
+    }
+    S1[b] = b1;
+    S2[b] = b2;
+    __syncthreads();
+    for (int off = 1; off < (int)blockDim.x; off <<= 1) {  // inclusive suffix sums
+        u64 v1 = S1[b], v2 = S2[b];
+        if (b + off < (int)blockDim.x) {
+            v1 = gl_add(v1, S1[b + off]);
+            v2 = gl_add(v2, S2[b + off]);
+        }
+        __syncthreads();
+        S1[b] = v1;
+        S2[b] = v2;
+        __syncthreads();
+    }
+    if (b < nblk) {
+        const u64 e = (u64)(b + 1) << logch;  // carry into block b: z^-e * sum over blocks after b
+        const u64 x1 = b + 1 < nblk ? S1[b + 1] : 0, x2 = b + 1 < nblk ? S2[b + 1] : 0;
+        carry[((u64)proof * nblk + b) * 2] = gl_mul(x1, gl_pow(P.zinv, e));
+        carry[((u64)proof * nblk + b) * 2 + 1] = gl_mul(x2, gl_pow(P.zginv, e));
     }
 }
 __device__ __forceinline__ int dpad(int i) { return i + i / OOD_R; }  // chunk stride R+1: no bank pile-up
@@ -529,8 +584,9 @@ void launch_deep(const u64* coef, const u64* hcoef, const DeepParams* dp, const 
     const int T = ood_threads(n), nblk = (int)(n / ((u64)T * OOD_R));
     int logch = 0;
     while ((1ULL << logch) < (u64)T * OOD_R) logch++;
-    hipLaunchKernelGGL(deep_carry_kernel, dim3((npoly + 63) / 64), dim3(64), 0, s, partial, dp, carry, nblk, logch,
-                       npoly);
+    int ct = 64;
+    while (ct < nblk) ct <<= 1;  // nblk <= 1024 (n <= 2^21, 2048 coefficients per block)
+    hipLaunchKernelGGL(deep_carry_kernel, dim3(npoly), dim3(ct), 0, s, partial, dp, carry, nblk, logch);
     hipLaunchKernelGGL(deep_final_kernel, dim3(nblk, npoly), dim3(T), 0, s, coef, hcoef, dp, carry, deep, logn);
     XFG_CHECK_LAUNCH();
 }

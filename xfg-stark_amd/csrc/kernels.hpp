@@ -43,16 +43,19 @@ void launch_interpolate(const u64* evals, u64 in_stride, u64* out, u64 out_strid
 // ---- Merkle (heap layout: nodes[1] = root, nodes[L + i] = leaf i) ----
 // LDE commitments store levels >= log2(beta) + 1 only: node_stride >= 2n; the subtree over rows
 // (2j, 2j+1) tops out at heap node n/2 + j; launch_tree_top(nodes, stride, n / 2, ...) finishes
-void launch_leaves_lde(const u64* lde, int nc, Digest* nodes, u64 node_stride, int npoly, int logn, int logbeta,
-                       hipStream_t s);
+// also merges each block's nodes a few levels up; returns the node count of the highest level
+// written (finish with launch_tree_top(nodes, stride, returned count, ...))
+u64 launch_leaves_lde(const u64* lde, int nc, Digest* nodes, u64 node_stride, int npoly, int logn, int logbeta,
+                      hipStream_t s);
 // recompute the local subtree heap (2 * beta digests, slot 1 = top, leaf t at beta + t) of LDE
 // rows entries[e] = proof << logn | m, for Merkle openings
 void launch_open_rows(const u64* lde, int nc, const u64* entries, u64 count, Digest* out, int logn, int logbeta,
                       hipStream_t s);
 // FRI layer leaves: row i = values at natural indices i + k*rows, k < 8 (coset-major source when
 // coset_major, else natural); all leaves stored at nodes[rows + i]
-void launch_fri_leaves(const u64* vals, u64 val_stride, bool coset_major, int logn, int logbeta, u64 rows,
-                       Digest* nodes, u64 node_stride, int npoly, hipStream_t s);
+// (returns the node count left for launch_tree_top, like launch_leaves_lde)
+u64 launch_fri_leaves(const u64* vals, u64 val_stride, bool coset_major, int logn, int logbeta, u64 rows,
+                      Digest* nodes, u64 node_stride, int npoly, hipStream_t s);
 // completes the tree above level `count` (nodes [count, 2count) present) up to the root
 void launch_tree_top(Digest* nodes, u64 node_stride, u64 count, int npoly, hipStream_t s);
 

@@ -638,8 +638,8 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     launch_interpolate(c->trace.p, n, c->coef.p, n, c->scratch.p, B * 7, logn, false, n, T, s);
     launch_lde(c->coef.p, n, c->lde.p, c->scratch.p, B * 7, logn, logbeta, T, s);
     stage_mark(c, 1);
-    launch_leaves_lde(c->lde.p, 7, c->tnodes.p, 2 * n, B, logn, logbeta, s);
-    launch_tree_top(c->tnodes.p, 2 * n, n / 2, B, s);
+    launch_tree_top(c->tnodes.p, 2 * n, launch_leaves_lde(c->lde.p, 7, c->tnodes.p, 2 * n, B, logn, logbeta, s), B,
+                    s);
     Digest* roots = c->h_roots.ensure(B);
     stage_mark(c, 2);
     ht.mark("launch1");
@@ -665,8 +665,8 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     launch_interpolate(c->ce.p, 2 * n, c->hcoef.p, n, c->scratch.p, B, logn + 1, true, n, T, s);
     launch_lde(c->hcoef.p, n, c->hlde.p, c->scratch.p, B, logn, logbeta, T, s);
     stage_mark(c, 4);
-    launch_leaves_lde(c->hlde.p, 1, c->hnodes.p, 2 * n, B, logn, logbeta, s);
-    launch_tree_top(c->hnodes.p, 2 * n, n / 2, B, s);
+    launch_tree_top(c->hnodes.p, 2 * n, launch_leaves_lde(c->hlde.p, 1, c->hnodes.p, 2 * n, B, logn, logbeta, s), B,
+                    s);
     stage_mark(c, 5);
     ht.mark("launch2");
     fetch_roots(c, c->hnodes.p, 2 * n, B, roots);
@@ -735,8 +735,8 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         const bool cm = (l == 0);
         const u64* src = cm ? c->f0.p : c->flayer[l].p;
         const u64 sstride = cm ? N : D[l];
-        launch_fri_leaves(src, sstride, cm, logn, logbeta, rows, c->fnodes[l].p, 2 * rows, B, s);
-        launch_tree_top(c->fnodes[l].p, 2 * rows, rows, B, s);
+        u64 top = launch_fri_leaves(src, sstride, cm, logn, logbeta, rows, c->fnodes[l].p, 2 * rows, B, s);
+        launch_tree_top(c->fnodes[l].p, 2 * rows, top, B, s);
         ht.mark("fri_launch");
         fetch_roots(c, c->fnodes[l].p, 2 * rows, B, roots);
         ht.mark("sync_fri");
