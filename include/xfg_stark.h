@@ -47,7 +47,8 @@ typedef enum {
     XFG_PROVER_ERROR = 6,        /* Winterfell prover error / unsupported options */
     XFG_DEVICE_ERROR = 7,        /* HIP runtime failure */
     XFG_BUFFER_TOO_SMALL = 8,
-    XFG_INVALID_ARGUMENT = 9
+    XFG_INVALID_ARGUMENT = 9,
+    XFG_VERIFY_FAILED = 10       /* proof rejected (verifier) or not a well-formed proof (parser) */
 } xfg_status;
 
 /* winterfell::ProofOptions (0.8) */
@@ -118,7 +119,43 @@ int xfg_prepare(xfg_ctx* ctx, uint32_t count, uint64_t trace_length, const xfg_o
 /* AIR constants from raw inputs (marshalling + Keccak, host); returns a validation status */
 int xfg_burn_air_consts(const xfg_burn_inputs* in, xfg_air_consts* out);
 
+/* ---- proofs: parsing and verification (host; no device needed) ---- */
+/* header of a parsed proof (StarkProof::from_bytes, winter-air 0.8) */
+typedef struct {
+    uint32_t trace_width;
+    uint64_t trace_length;
+    xfg_options options;
+    uint32_t num_unique_queries;
+    uint32_t num_fri_layers;
+    uint32_t remainder_len;     /* FRI remainder coefficients */
+    uint64_t pow_nonce;
+    uint8_t trace_root[32];
+    uint8_t constraint_root[32];
+    uint64_t ood_trace[14];     /* T_c(z), T_c(z g) interleaved */
+    uint64_t ood_composition;   /* H(z) */
+    size_t size;                /* bytes consumed == len for a well-formed proof */
+} xfg_proof_info;
+
+/* StarkProof::from_bytes <- src/burn_mint_prover.rs:224-227 (to_bytes), src/bin/xfg-stark-cli.rs:533-558
+ * structural parse of proof bytes; XFG_VERIFY_FAILED + ProofDeserializationError text on bad input */
+int xfg_proof_parse(const uint8_t* proof, size_t len, xfg_proof_info* info, char* err, size_t err_len);
+
+/* winterfell::verify::<XfgBurnMintAir, Blake3_256, DefaultRandomCoin> with
+ * AcceptableOptions::OptionSet([*acceptable])  <- XfgBurnMintVerifier::verify_with_public_inputs /
+ * verify_with_winterfell, src/burn_mint_verifier.rs:186-203, 265-283. The statement is the AIR
+ * constants (12 public inputs + nullifier + commitment, see xfg_burn_air_consts). XFG_OK = accepted;
+ * XFG_VERIFY_FAILED = rejected, err receives the VerifierError (Debug form, e.g.
+ * "InconsistentOodConstraintEvaluations"). */
+int xfg_verify(const uint8_t* proof, size_t len, const xfg_air_consts* air, const xfg_options* acceptable, char* err,
+               size_t err_len);
+/* BatchBurnMintVerifier::verify_batch <- src/burn_mint_verifier.rs:386-408 (and batch_verify
+ * :326-338): results[i] = xfg_verify status of proof i; `threads` host threads (0 = all cores) */
+int xfg_verify_batch(uint32_t count, const uint8_t* const* proofs, const size_t* lens, const xfg_air_consts* airs,
+                     const xfg_options* acceptable, int* results, uint32_t threads);
+
 /* ---- instrumentation (benchmarks / parity tests) ---- */
+/* host BLAKE3 of the library (any length), for self-tests */
+int xfg_selftest_blake3(const uint8_t* in, size_t len, uint8_t out[32]);
 /* host-side field arithmetic of the library (mul, add, sub) for self-tests; canonical inputs */
 int xfg_selftest_field(uint64_t a, uint64_t b, uint64_t* out3);
 /* per-stage device milliseconds of the last prove call when timing is enabled (returns count) */

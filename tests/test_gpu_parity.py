@@ -221,6 +221,25 @@ def test_large_traces_verify(prover, logn, blowup):
     assert O.verify(oracle_air(kw), p1, O.options(blowup=blowup)) == 0
 
 
+@pytest.mark.parametrize("n,kw", [(2048, dict(fri_remainder_max_degree=255)), (1024, dict(fri_remainder_max_degree=7)),
+                                  (512, dict(num_queries=24, grinding_factor=0)), (256, dict(blowup_factor=16))])
+def test_other_options_match_oracle_and_verify(prover, n, kw):
+    """non-default ProofOptions (long multi-chunk FRI remainder commitment, small remainder, fewer
+    queries / no grinding, blowup 16): GPU bytes == oracle bytes, and the product verifier accepts"""
+    import xfgstark
+    o = xfgstark.ProofOptions.reference()
+    for k, v in kw.items():
+        setattr(o, k, v)
+    prover._options = o
+    kws = synthetic.burn_inputs(900 + n)
+    proof = prover.prove_burn_mint(**kws, trace_length=n).to_bytes()
+    oo = O.options(num_queries=o.num_queries, blowup=o.blowup_factor, grinding=o.grinding_factor,
+                   fri_rem_max_deg=o.fri_remainder_max_degree)
+    st, want = O.prove(oracle_air(kws), n, oo)
+    assert st == 0 and proof == want
+    assert xfgstark.XfgBurnMintVerifier(proof_options=o).verify_burn_mint(proof, **kws)
+
+
 def test_rejects_options_the_reference_rejects(prover):
     import xfgstark
     kw = synthetic.burn_inputs(3)

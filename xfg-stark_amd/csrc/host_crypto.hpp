@@ -1,6 +1,7 @@
 // Host-side hashing for the transcript and AIR constants (product code; the parity oracle under
 // oracle/ is a separate, independent C restatement).
-//  - BLAKE3 of <= 1024 bytes (one chunk): Fiat-Shamir seed (Context || public inputs, 160 B),
+//  - BLAKE3 (any length; transcript inputs are one chunk except FRI remainders > 128 elements):
+//    Fiat-Shamir seed (Context || public inputs, 160 B),
 //    OOD frame hash (112 B), FRI remainder commitment, coin draws.
 //  - Keccak-256 (sha3::Keccak256): AIR constants, reference src/burn_mint_air.rs:124-202 and
 //    src/burn_mint_prover.rs:211-221 -- computed once per proof instead of once per
@@ -8,6 +9,7 @@
 #pragma once
 #include <stdint.h>
 #include <string.h>
+#include <array>
 #include <vector>
 #include "blake3.hpp"
 
@@ -17,23 +19,79 @@ inline void le_words(const uint8_t* b, size_t len, uint32_t m[16]) {
     for (int i = 0; i < 16; i++) m[i] = 0;
     for (size_t i = 0; i < len; i++) m[i / 4] |= (uint32_t)b[i] << (8 * (i % 4));
 }
-inline Digest blake3_bytes(const uint8_t* in, size_t len) {
-    // single chunk (<= 1024 bytes): blocks chained with CHUNK_START on the first and
-    // CHUNK_END | ROOT on the last
-    uint32_t cv[8] = {XFG_B3_IV0, XFG_B3_IV1, XFG_B3_IV2, XFG_B3_IV3, XFG_B3_IV4, XFG_B3_IV5, XFG_B3_IV6, XFG_B3_IV7};
-    size_t nblocks = len == 0 ? 1 : (len + 63) / 64;
-    for (size_t b = 0; b < nblocks; b++) {
-        size_t off = b * 64, bl = len == 0 ? 0 : (len - off < 64 ? len - off : 64);
-        uint32_t m[16];
-        le_words(in + off, bl, m);
-        uint32_t flags = (b == 0 ? B3_CHUNK_START : 0) | (b == nblocks - 1 ? (B3_CHUNK_END | B3_ROOT) : 0);
-        uint32_t out[8];
-        b3_compress(cv, m, (uint32_t)bl, 0, flags, out);
-        memcpy(cv, out, sizeof cv);
+// BLAKE3 (hash mode, any length): 1024-byte chunks chained block by block; chunk chaining values
+// merged in the left-balanced binary tree of the BLAKE3 spec (PARENT nodes), ROOT on the last
+// compression. One-chunk inputs (every transcript hash except long FRI remainders) take the
+// first branch only.
+struct B3Output {  // a compression whose flags are not final yet (ROOT is added at the very end)
+    uint32_t cv[8], m[16], len, flags;
+    uint64_t counter;
+    void chaining(uint32_t out[8]) const {
+        uint32_t mm[16];
+        memcpy(mm, m, sizeof mm);
+        b3_compress(cv, mm, len, counter, flags, out);
     }
-    Digest d;
-    memcpy(d.w, cv, sizeof cv);
-    return d;
+    Digest root() const {
+        uint32_t mm[16];
+        memcpy(mm, m, sizeof mm);
+        Digest d;
+        b3_compress(cv, mm, len, counter, flags | B3_ROOT, d.w);
+        return d;
+    }
+};
+inline B3Output b3_chunk(const uint8_t* in, size_t len, uint64_t counter) {
+    B3Output o;
+    const uint32_t iv[8] = {XFG_B3_IV0, XFG_B3_IV1, XFG_B3_IV2, XFG_B3_IV3, XFG_B3_IV4, XFG_B3_IV5, XFG_B3_IV6, XFG_B3_IV7};
+    memcpy(o.cv, iv, sizeof iv);
+    const size_t nblocks = len == 0 ? 1 : (len + 63) / 64;
+    for (size_t b = 0; b < nblocks; b++) {
+        const size_t off = b * 64, bl = len == 0 ? 0 : (len - off < 64 ? len - off : 64);
+        le_words(in + off, bl, o.m);
+        o.len = (uint32_t)bl;
+        o.counter = counter;
+        o.flags = (b == 0 ? B3_CHUNK_START : 0) | (b == nblocks - 1 ? B3_CHUNK_END : 0);
+        if (b + 1 < nblocks) {
+            uint32_t out[8];
+            o.chaining(out);
+            memcpy(o.cv, out, sizeof out);
+        }
+    }
+    return o;
+}
+inline B3Output b3_parent(const uint32_t l[8], const uint32_t r[8]) {
+    B3Output o;
+    const uint32_t iv[8] = {XFG_B3_IV0, XFG_B3_IV1, XFG_B3_IV2, XFG_B3_IV3, XFG_B3_IV4, XFG_B3_IV5, XFG_B3_IV6, XFG_B3_IV7};
+    memcpy(o.cv, iv, sizeof iv);
+    memcpy(o.m, l, 32);
+    memcpy(o.m + 8, r, 32);
+    o.len = 64;
+    o.counter = 0;
+    o.flags = B3_PARENT;
+    return o;
+}
+inline Digest blake3_bytes(const uint8_t* in, size_t len) {
+    const size_t nchunks = len == 0 ? 1 : (len + 1023) / 1024;
+    std::vector<std::array<uint32_t, 8>> stack;
+    for (size_t c = 0; c + 1 < nchunks; c++) {
+        std::array<uint32_t, 8> cv;
+        b3_chunk(in + c * 1024, 1024, c).chaining(cv.data());
+        for (uint64_t total = c + 1; (total & 1) == 0; total >>= 1) {  // add_chunk_chaining_value
+            std::array<uint32_t, 8> merged;
+            b3_parent(stack.back().data(), cv.data()).chaining(merged.data());
+            stack.pop_back();
+            cv = merged;
+        }
+        stack.push_back(cv);
+    }
+    const size_t last = (nchunks - 1) * 1024;
+    B3Output out = b3_chunk(in + last, len - last, nchunks - 1);
+    while (!stack.empty()) {
+        uint32_t cv[8];
+        out.chaining(cv);
+        out = b3_parent(stack.back().data(), cv);
+        stack.pop_back();
+    }
+    return out.root();
 }
 inline void digest_bytes(const Digest& d, uint8_t out[32]) {
     for (int i = 0; i < 8; i++)

@@ -1,0 +1,462 @@
+// Proof parsing (StarkProof::from_bytes) and the STARK verifier for the burn AIR, host C++.
+//
+// Replaces winterfell::verify::<XfgBurnMintAir, Blake3_256, DefaultRandomCoin> as called by the
+// reference verifier (src/burn_mint_verifier.rs:265-283; batch loops :326-338, :386-408). The
+// statement is the 12 public inputs plus the two Keccak-derived AIR constants (nullifier,
+// commitment): the corrected AIR binds the prover's secret through them,
+// so the verifier takes them as inputs instead of rebuilding the AIR from a fixed secret.
+// Product code: independent of the oracle under oracle/ (which is test infrastructure only).
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "host_common.hpp"
+#include "kernels.hpp"
+
+namespace xfg {
+
+// ------------------------------------------------------------------ byte reader
+struct Reader {
+    const uint8_t* p;
+    size_t n, off = 0;
+    bool bad = false;
+    const uint8_t* take(size_t k) {
+        if (bad || k > n - off) {
+            bad = true;
+            return nullptr;
+        }
+        const uint8_t* q = p + off;
+        off += k;
+        return q;
+    }
+    u64 u(int bytes) {
+        const uint8_t* q = take((size_t)bytes);
+        u64 v = 0;
+        if (q)
+            for (int i = 0; i < bytes; i++) v |= (u64)q[i] << (8 * i);
+        return v;
+    }
+};
+struct Span {
+    const uint8_t* p = nullptr;
+    size_t n = 0;
+    u64 elem(size_t i) const {
+        u64 v;
+        memcpy(&v, p + 8 * i, 8);
+        return v;
+    }
+};
+// BatchMerkleProof::serialize_nodes: u8 vector count, then per vector u8 count + digests
+struct Paths {
+    std::vector<std::vector<Digest>> vecs;
+};
+
+// StarkProof fields in wire order (DESIGN.md "Proof format")
+struct ParsedProof {
+    u64 width = 0, aux = 0, logn = 0;
+    Opts o{};
+    u64 num_unique = 0;
+    std::vector<Digest> com;  // trace root, constraint root, FRI layer roots, remainder commitment
+    Span trace_rows, constraint_rows, ood, fri_rem;
+    Paths trace_paths, constraint_paths;
+    u64 hz = 0;
+    std::vector<Span> fri_vals;
+    std::vector<Paths> fri_paths;
+    u64 partitions = 0, nonce = 0;
+    size_t size = 0;
+};
+
+static bool read_paths(Reader& r, size_t len, Paths& out) {
+    const uint8_t* q = r.take(len);
+    if (!q) return false;
+    Reader s{q, len};
+    const u64 m = s.u(1);
+    out.vecs.resize(m);
+    for (u64 i = 0; i < m; i++) {
+        const u64 c = s.u(1);
+        const uint8_t* d = s.take(c * 32);
+        if (!d) return false;
+        out.vecs[i].resize(c);
+        memcpy(out.vecs[i].data(), d, c * 32);
+    }
+    return !s.bad && s.off == len;
+}
+static bool read_span(Reader& r, int len_bytes, Span& s) {
+    s.n = r.u(len_bytes);
+    s.p = r.take(s.n);
+    return !r.bad;
+}
+
+// returns "" on success, else the ProofDeserializationError text
+static std::string parse_proof(const uint8_t* bytes, size_t len, ParsedProof& pf) {
+    Reader r{bytes, len};
+    pf.width = r.u(1);
+    pf.aux = r.u(1);
+    pf.logn = r.u(1);
+    const u64 meta = r.u(2);
+    r.take(meta);
+    const u64 mlen = r.u(1), modulus = r.u(8);
+    pf.o.q = r.u(1);
+    pf.o.beta = r.u(1);
+    pf.o.grind = r.u(1);
+    pf.o.ext = r.u(1);
+    pf.o.fold = r.u(1);
+    pf.o.remdeg = r.u(1);
+    if (r.bad) return "ProofDeserializationError(\"context: unexpected end of input\")";
+    if (mlen != 8 || modulus != xfg::P) return "InconsistentBaseField";
+    if (pf.logn < 3 || pf.logn > 32) return "ProofDeserializationError(\"context: invalid trace length\")";
+    pf.num_unique = r.u(1);
+    const u64 clen = r.u(2);
+    const uint8_t* c = r.take(clen);
+    if (!c || clen % 32) return "ProofDeserializationError(\"commitments\")";
+    pf.com.resize(clen / 32);
+    memcpy(pf.com.data(), c, clen);
+    if (r.u(1) != 1) return "ProofDeserializationError(\"trace queries: expected one segment\")";
+    if (!read_span(r, 4, pf.trace_rows)) return "ProofDeserializationError(\"trace queries\")";
+    const u64 tpl = r.u(4);
+    if (r.bad || !read_paths(r, tpl, pf.trace_paths)) return "ProofDeserializationError(\"trace query paths\")";
+    if (!read_span(r, 4, pf.constraint_rows)) return "ProofDeserializationError(\"constraint queries\")";
+    const u64 cpl = r.u(4);
+    if (r.bad || !read_paths(r, cpl, pf.constraint_paths))
+        return "ProofDeserializationError(\"constraint query paths\")";
+    Span hz;
+    if (!read_span(r, 2, pf.ood) || !read_span(r, 2, hz)) return "ProofDeserializationError(\"OOD frame\")";
+    if (pf.ood.n < 1 || pf.ood.p[0] != 2 || (pf.ood.n - 1) % 16 || hz.n != 8)
+        return "ProofDeserializationError(\"OOD frame layout\")";
+    pf.ood.p += 1;
+    pf.ood.n -= 1;
+    pf.hz = hz.elem(0);
+    const u64 nl = r.u(1);
+    pf.fri_vals.resize(nl);
+    pf.fri_paths.resize(nl);
+    for (u64 l = 0; l < nl; l++) {
+        if (!read_span(r, 4, pf.fri_vals[l])) return "ProofDeserializationError(\"FRI layer values\")";
+        const u64 pl = r.u(4);
+        if (r.bad || !read_paths(r, pl, pf.fri_paths[l])) return "ProofDeserializationError(\"FRI layer paths\")";
+    }
+    if (!read_span(r, 2, pf.fri_rem) || pf.fri_rem.n % 8) return "ProofDeserializationError(\"FRI remainder\")";
+    pf.partitions = r.u(1);
+    pf.nonce = r.u(8);
+    if (r.bad) return "ProofDeserializationError(\"unexpected end of input\")";
+    if (r.off != len) return "ProofDeserializationError(\"trailing bytes\")";
+    pf.size = r.off;
+    return "";
+}
+
+// ------------------------------------------------------------------ batch Merkle root
+// BatchMerkleProof::get_root: the node vectors must hold exactly the siblings the opening plan of
+// `idx` asks for; every node on the way to the root is then recomputed.
+static bool batch_root(const std::vector<u64>& idx, const std::vector<Digest>& leaf, const Paths& paths, u64 L,
+                       Digest& root) {
+    BatchOpening plan;
+    plan_batch_opening(idx, L, plan);
+    if (plan.size() != paths.vecs.size()) return false;
+    std::unordered_map<u64, Digest> known;
+    known.reserve(4 * (idx.size() + 1) * (ilog2(L) + 1));
+    for (size_t i = 0; i < idx.size(); i++) known[L + idx[i]] = leaf[i];
+    for (size_t i = 0; i < plan.size(); i++) {
+        if (paths.vecs[i].size() != plan.len[i]) return false;
+        for (unsigned k = 0; k < plan.len[i]; k++) known[plan.row(i)[k]] = paths.vecs[i][k];
+    }
+    std::vector<u64> level;
+    for (u64 i : idx) level.push_back(L + i);
+    std::sort(level.begin(), level.end());
+    level.erase(std::unique(level.begin(), level.end()), level.end());
+    while (!(level.size() == 1 && level[0] == 1)) {
+        std::vector<u64> up;
+        for (u64 x : level) {
+            const u64 p = x >> 1;
+            if (!up.empty() && up.back() == p) continue;
+            auto a = known.find(2 * p), b = known.find(2 * p + 1);
+            if (a == known.end() || b == known.end()) return false;
+            known[p] = b3_merge(a->second, b->second);
+            up.push_back(p);
+        }
+        level.swap(up);
+    }
+    root = known[1];
+    return true;
+}
+static bool same(const Digest& a, const Digest& b) { return !memcmp(a.w, b.w, 32); }
+static Digest leaf_hash(const uint8_t* bytes, size_t len) { return blake3_bytes(bytes, len); }
+
+// ------------------------------------------------------------------ burn AIR at a point
+// evaluate_transition (src/burn_mint_air.rs:335-378, corrected AIR A.2) and the 8 assertions
+// (:380-395, final state assertion at n - 1)
+static void air_transition(const AirConst& a, const u64 cur[7], const u64 nxt[7], u64 r[7]) {
+    const u64 std_burn = 8000000ULL, large = gl_mul(std_burn, 1000);
+    r[0] = gl_mul(gl_sub(cur[0], std_burn), gl_sub(cur[0], large));
+    r[1] = gl_sub(cur[1], cur[0]);
+    r[2] = gl_sub(cur[2], a.pub[2]);
+    r[3] = gl_sub(cur[3], a.pub[3]);
+    const u64 d = gl_sub(nxt[4], cur[4]);
+    r[4] = gl_mul(d, gl_sub(d, 1));
+    r[5] = gl_sub(cur[5], a.nullifier);
+    r[6] = gl_sub(cur[6], a.commitment);
+}
+
+// FRI apply_drp on one row (folding 8, domain offset 7): interpolate the 8 values on the coset
+// x * <w_8> and evaluate at alpha
+static u64 fold_row(const u64 v[8], u64 x, u64 alpha) {
+    // coefficients of the degree < 8 interpolant in (X / x): c = iDFT_8(v) / 8
+    const u64 w8 = gl_root(3);
+    u64 c[8];
+    u64 winv = gl_inv(w8), inv8 = gl_inv(8);
+    for (int k = 0; k < 8; k++) {
+        u64 s = 0, wk = gl_pow(winv, (u64)k), p = 1;
+        for (int j = 0; j < 8; j++) {
+            s = gl_add(s, gl_mul(v[j], p));
+            p = gl_mul(p, wk);
+        }
+        c[k] = gl_mul(s, inv8);
+    }
+    const u64 t = gl_mul(alpha, gl_inv(x));
+    u64 r = 0;
+    for (int k = 7; k >= 0; k--) r = gl_add(gl_mul(r, t), c[k]);
+    return r;
+}
+
+// returns "" when the proof verifies, else the VerifierError (Debug form)
+static std::string verify_proof(const uint8_t* bytes, size_t len, const AirConst& air, const Opts& acceptable) {
+    ParsedProof pf;
+    std::string e = parse_proof(bytes, len, pf);
+    if (!e.empty()) return e;
+    if (pf.width != 7 || pf.aux != 0) return "InconsistentTraceWidth";
+    const Opts& o = pf.o;
+    if (memcmp(&o, &acceptable, sizeof o)) return "UnacceptableProofOptions";  // AcceptableOptions::OptionSet
+    const u64 n = 1ULL << pf.logn;
+    if (check_options(n, o)) return "UnacceptableProofOptions";
+    const u64 beta = o.beta, N = n * beta, depthN = pf.logn + ilog2(beta);
+    const unsigned nl = num_fri_layers(N, o);
+    if (pf.com.size() != 3 + nl || pf.fri_vals.size() != nl || pf.partitions != 0 || pf.num_unique == 0 ||
+        pf.ood.n != 14 * 8)
+        return "ProofDeserializationError(\"inconsistent proof structure\")";
+    const u64 nu = pf.num_unique;
+    if (pf.trace_rows.n != nu * 7 * 8 || pf.constraint_rows.n != nu * 8)
+        return "ProofDeserializationError(\"query count\")";
+
+    // ---- transcript
+    u64 seed[20];
+    context_elements(n, o, seed);
+    memcpy(seed + 8, air.pub, 12 * 8);
+    Coin coin;
+    coin.init(seed, 20);
+    coin.reseed(pf.com[0]);
+    u64 alpha[7], bc[8];
+    for (auto& x : alpha)
+        if (!coin.draw(x)) return "RandomCoinError";
+    for (auto& x : bc)
+        if (!coin.draw(x)) return "RandomCoinError";
+    coin.reseed(pf.com[1]);
+    u64 z;
+    if (!coin.draw(z)) return "RandomCoinError";
+    const u64 g = gl_root((unsigned)pf.logn), zg = gl_mul(z, g), g_last = gl_pow(g, n - 1);
+    u64 ood[14];
+    for (int k = 0; k < 14; k++) ood[k] = pf.ood.elem(k);
+
+    // ---- OOD consistency: H(z) == sum alpha_i r_i(z) Z_t(z)^-1 + boundary terms
+    {
+        u64 cur[7], nxt[7], rr[7];
+        for (int c = 0; c < 7; c++) {
+            cur[c] = ood[2 * c];
+            nxt[c] = ood[2 * c + 1];
+        }
+        air_transition(air, cur, nxt, rr);
+        u64 t = 0;
+        for (int c = 0; c < 7; c++) t = gl_add(t, gl_mul(alpha[c], rr[c]));
+        const u64 zn1 = gl_sub(gl_pow(z, n), 1);
+        if (zn1 == 0 || z == 1 || z == g_last) return "InconsistentOodConstraintEvaluations";
+        u64 ev = gl_mul(gl_mul(t, gl_sub(z, g_last)), gl_inv(zn1));
+        const u64 v0[7] = {air.pub[0], air.pub[1], air.pub[2], air.pub[3], 0, air.nullifier, air.commitment};
+        u64 b0 = 0;
+        for (int c = 0; c < 7; c++) b0 = gl_add(b0, gl_mul(bc[c], gl_sub(cur[c], v0[c])));
+        const u64 b1 = gl_mul(bc[7], gl_sub(cur[4], 3));
+        ev = gl_add(ev, gl_mul(b0, gl_inv(gl_sub(z, 1))));
+        ev = gl_add(ev, gl_mul(b1, gl_inv(gl_sub(z, g_last))));
+        if (ev != pf.hz) return "InconsistentOodConstraintEvaluations";
+    }
+    coin.reseed(hash_elements(ood, 14));
+    coin.reseed(hash_elements(&pf.hz, 1));
+    u64 dc[7], gam;
+    for (auto& x : dc)
+        if (!coin.draw(x)) return "RandomCoinError";
+    if (!coin.draw(gam)) return "RandomCoinError";
+    std::vector<u64> falpha(nl);
+    for (unsigned l = 0; l <= nl; l++) {
+        coin.reseed(pf.com[2 + l]);
+        u64 a;
+        if (!coin.draw(a)) return "RandomCoinError";
+        if (l < nl) falpha[l] = a;
+    }
+    // ---- proof of work + query positions
+    {
+        Digest h = merge_with_int(coin.seed, pf.nonce);
+        if (tz64((u64)h.w[0] | ((u64)h.w[1] << 32)) < o.grind) return "QuerySeedProofOfWorkVerificationFailed";
+    }
+    coin.reseed_int(pf.nonce);
+    std::vector<u64> pos(o.q);
+    for (auto& x : pos) {
+        Digest h = coin.next();
+        x = ((u64)h.w[0] | ((u64)h.w[1] << 32)) & (N - 1);
+    }
+    std::sort(pos.begin(), pos.end());
+    pos.erase(std::unique(pos.begin(), pos.end()), pos.end());
+    if (pos.size() != nu) return "ProofDeserializationError(\"number of unique queries\")";
+
+    // ---- trace / constraint openings
+    std::vector<Digest> leaves(nu);
+    Digest root;
+    for (u64 i = 0; i < nu; i++) leaves[i] = leaf_hash(pf.trace_rows.p + i * 56, 56);
+    if (!batch_root(pos, leaves, pf.trace_paths, N, root) || !same(root, pf.com[0]))
+        return "TraceQueryDoesNotMatchCommitment";
+    for (u64 i = 0; i < nu; i++) leaves[i] = leaf_hash(pf.constraint_rows.p + i * 8, 8);
+    if (!batch_root(pos, leaves, pf.constraint_paths, N, root) || !same(root, pf.com[1]))
+        return "ConstraintQueryDoesNotMatchCommitment";
+
+    // ---- DEEP composition at the query points
+    std::vector<u64> ev(nu);
+    const u64 wN = gl_root((unsigned)depthN);
+    for (u64 i = 0; i < nu; i++) {
+        const u64 x = gl_mul(GEN, gl_pow(wN, pos[i]));
+        u64 s1 = 0, s2 = 0;
+        for (int c = 0; c < 7; c++) {
+            const u64 tx = pf.trace_rows.elem(i * 7 + c);
+            s1 = gl_add(s1, gl_mul(dc[c], gl_sub(tx, ood[2 * c])));
+            s2 = gl_add(s2, gl_mul(dc[c], gl_sub(tx, ood[2 * c + 1])));
+        }
+        const u64 izx = gl_inv(gl_sub(x, z)), izgx = gl_inv(gl_sub(x, zg));
+        u64 d = gl_add(gl_mul(s1, izx), gl_mul(s2, izgx));
+        d = gl_add(d, gl_mul(gl_mul(gam, gl_sub(pf.constraint_rows.elem(i), pf.hz)), izx));
+        ev[i] = d;
+    }
+
+    // ---- FRI: each layer's openings, folding consistency, remainder
+    std::vector<u64> cur = pos;
+    u64 D = N;
+    for (unsigned l = 0; l < nl; l++) {
+        const u64 rows = D / 8;
+        std::vector<u64> fp = fold_positions(cur, rows);
+        const Span& vals = pf.fri_vals[l];
+        if (vals.n != fp.size() * 64) return "FriVerificationFailed(InvalidLayerCommitment)";
+        std::vector<Digest> lv(fp.size());
+        for (size_t i = 0; i < fp.size(); i++) lv[i] = leaf_hash(vals.p + i * 64, 64);
+        if (!batch_root(fp, lv, pf.fri_paths[l], rows, root) || !same(root, pf.com[2 + l]))
+            return "FriVerificationFailed(LayerCommitmentMismatch)";
+        for (size_t i = 0; i < cur.size(); i++) {
+            const u64 ri = cur[i] & (rows - 1), k = cur[i] / rows;
+            const size_t at = std::find(fp.begin(), fp.end(), ri) - fp.begin();
+            if (vals.elem(at * 8 + k) != ev[i]) return "FriVerificationFailed(InvalidLayerFolding)";
+        }
+        const u64 wD = gl_root(ilog2(D));
+        std::vector<u64> nev(fp.size());
+        for (size_t i = 0; i < fp.size(); i++) {
+            u64 v[8];
+            for (int k = 0; k < 8; k++) v[k] = vals.elem(i * 8 + k);
+            nev[i] = fold_row(v, gl_mul(GEN, gl_pow(wD, fp[i])), falpha[l]);
+        }
+        cur.swap(fp);
+        ev.swap(nev);
+        D = rows;
+    }
+    const u64 rl = pf.fri_rem.n / 8;
+    if (rl == 0 || rl != D / beta) return "FriVerificationFailed(InvalidRemainderFolding)";
+    std::vector<u64> rem(rl);
+    for (u64 i = 0; i < rl; i++) rem[i] = pf.fri_rem.elem(i);
+    if (!same(hash_elements(rem.data(), rl), pf.com[2 + nl])) return "FriVerificationFailed(RemainderCommitmentMismatch)";
+    const u64 wD = gl_root(ilog2(D));
+    for (size_t i = 0; i < cur.size(); i++) {
+        const u64 x = gl_mul(GEN, gl_pow(wD, cur[i]));
+        u64 r = 0;
+        for (u64 k = rl; k-- > 0;) r = gl_add(gl_mul(r, x), rem[k]);
+        if (r != ev[i]) return "FriVerificationFailed(InvalidRemainderFolding)";
+    }
+    return "";
+}
+
+static AirConst air_of(const xfg_air_consts* a) {
+    AirConst c;
+    memset(&c, 0, sizeof c);
+    memcpy(c.pub, a->pub_inputs, sizeof a->pub_inputs);
+    c.nullifier = a->nullifier;
+    c.commitment = a->commitment;
+    return c;
+}
+static void put_err(const std::string& e, char* buf, size_t len) {
+    if (!buf || !len) return;
+    size_t k = std::min(len - 1, e.size());
+    memcpy(buf, e.data(), k);
+    buf[k] = 0;
+}
+
+}  // namespace xfg
+
+using namespace xfg;
+
+extern "C" {
+
+int xfg_proof_parse(const uint8_t* proof, size_t len, xfg_proof_info* info, char* err, size_t err_len) {
+    if (!proof || !info) return XFG_INVALID_ARGUMENT;
+    ParsedProof pf;
+    std::string e = parse_proof(proof, len, pf);
+    put_err(e, err, err_len);
+    if (!e.empty()) return XFG_VERIFY_FAILED;
+    memset(info, 0, sizeof *info);
+    info->trace_width = (uint32_t)pf.width;
+    info->trace_length = 1ULL << pf.logn;
+    info->options.num_queries = (uint32_t)pf.o.q;
+    info->options.blowup_factor = (uint32_t)pf.o.beta;
+    info->options.grinding_factor = (uint32_t)pf.o.grind;
+    info->options.field_extension = (uint32_t)pf.o.ext;
+    info->options.fri_folding_factor = (uint32_t)pf.o.fold;
+    info->options.fri_remainder_max_degree = (uint32_t)pf.o.remdeg;
+    info->num_unique_queries = (uint32_t)pf.num_unique;
+    info->num_fri_layers = (uint32_t)pf.fri_vals.size();
+    info->remainder_len = (uint32_t)(pf.fri_rem.n / 8);
+    info->pow_nonce = pf.nonce;
+    info->size = pf.size;
+    for (size_t i = 0; i < 2 && i < pf.com.size(); i++) memcpy(i ? info->constraint_root : info->trace_root, pf.com[i].w, 32);
+    for (int k = 0; k < 14; k++) info->ood_trace[k] = pf.ood.elem(k);
+    info->ood_composition = pf.hz;
+    return XFG_OK;
+}
+
+int xfg_verify(const uint8_t* proof, size_t len, const xfg_air_consts* air, const xfg_options* acceptable, char* err,
+               size_t err_len) {
+    if (!proof || !air || !acceptable) return XFG_INVALID_ARGUMENT;
+    std::string e;
+    try {
+        e = verify_proof(proof, len, air_of(air), to_opts(acceptable));
+    } catch (const std::exception& x) {
+        e = std::string("ProofDeserializationError(\"") + x.what() + "\")";
+    }
+    put_err(e, err, err_len);
+    return e.empty() ? XFG_OK : XFG_VERIFY_FAILED;
+}
+
+int xfg_selftest_blake3(const uint8_t* in, size_t len, uint8_t out[32]) {
+    if ((!in && len) || !out) return XFG_INVALID_ARGUMENT;
+    Digest d = blake3_bytes(in, len);
+    digest_bytes(d, out);
+    return XFG_OK;
+}
+
+int xfg_verify_batch(uint32_t count, const uint8_t* const* proofs, const size_t* lens, const xfg_air_consts* airs,
+                     const xfg_options* acceptable, int* results, uint32_t threads) {
+    if (!proofs || !lens || !airs || !acceptable || !results) return XFG_INVALID_ARGUMENT;
+    unsigned nt = threads ? threads : std::max(1u, std::thread::hardware_concurrency());
+    nt = std::min<unsigned>(nt, std::max<uint32_t>(1, count));
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; t++)
+        th.emplace_back([&, t] {
+            for (uint32_t i = t; i < count; i += nt)
+                results[i] = proofs[i] ? xfg_verify(proofs[i], lens[i], &airs[i], acceptable, nullptr, 0)
+                                       : XFG_INVALID_ARGUMENT;
+        });
+    for (auto& x : th) x.join();
+    return XFG_OK;
+}
+
+}  // extern "C"

@@ -21,7 +21,8 @@ if not os.path.exists(LIB_PATH):
 _lib = C.CDLL(LIB_PATH)
 
 STATUS = {0: "OK", 1: "INVALID_BURN_AMOUNT", 2: "MINT_MISMATCH", 3: "ZERO_TX_HASH", 4: "BAD_RECIPIENT_LEN",
-          5: "SHORT_SECRET", 6: "PROVER_ERROR", 7: "DEVICE_ERROR", 8: "BUFFER_TOO_SMALL", 9: "INVALID_ARGUMENT"}
+          5: "SHORT_SECRET", 6: "PROVER_ERROR", 7: "DEVICE_ERROR", 8: "BUFFER_TOO_SMALL", 9: "INVALID_ARGUMENT",
+          10: "VERIFY_FAILED"}
 
 
 class _Options(C.Structure):
@@ -39,6 +40,13 @@ class _BurnInputs(C.Structure):
 
 class _AirConsts(C.Structure):
     _fields_ = [("pub_inputs", C.c_uint64 * 12), ("nullifier", C.c_uint64), ("commitment", C.c_uint64)]
+
+
+class _ProofInfo(C.Structure):
+    _fields_ = [("trace_width", C.c_uint32), ("trace_length", C.c_uint64), ("options", _Options),
+                ("num_unique_queries", C.c_uint32), ("num_fri_layers", C.c_uint32), ("remainder_len", C.c_uint32),
+                ("pow_nonce", C.c_uint64), ("trace_root", C.c_uint8 * 32), ("constraint_root", C.c_uint8 * 32),
+                ("ood_trace", C.c_uint64 * 14), ("ood_composition", C.c_uint64), ("size", C.c_size_t)]
 
 
 _u64p = C.POINTER(C.c_uint64)
@@ -60,6 +68,11 @@ _lib.xfg_prove_batch_submit.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(_BurnI
                                          C.POINTER(_Options), C.POINTER(_u8p), C.POINTER(C.c_size_t),
                                          C.POINTER(C.c_int), C.POINTER(C.c_uint64)]
 _lib.xfg_batch_wait.argtypes = [C.c_void_p, C.c_uint64]
+_lib.xfg_proof_parse.argtypes = [_u8p, C.c_size_t, C.POINTER(_ProofInfo), C.c_char_p, C.c_size_t]
+_lib.xfg_verify.argtypes = [_u8p, C.c_size_t, C.POINTER(_AirConsts), C.POINTER(_Options), C.c_char_p, C.c_size_t]
+_lib.xfg_verify_batch.argtypes = [C.c_uint32, C.POINTER(_u8p), C.POINTER(C.c_size_t), C.POINTER(_AirConsts),
+                                  C.POINTER(_Options), C.POINTER(C.c_int), C.c_uint32]
+_lib.xfg_selftest_blake3.argtypes = [_u8p, C.c_size_t, _u8p]
 _lib.xfg_prepare.argtypes = [C.c_void_p, C.c_uint32, C.c_uint64, C.POINTER(_Options)]
 _lib.xfg_burn_air_consts.argtypes = [C.POINTER(_BurnInputs), C.POINTER(_AirConsts)]
 _lib.xfg_set_timing.argtypes = [C.c_void_p, C.c_int]
@@ -116,20 +129,148 @@ class ProofOptions:
                 "{0.fri_folding_factor}, fri_remainder_max_degree={0.fri_remainder_max_degree})").format(self)
 
 
+def _bytes_ptr(b):
+    return C.cast(C.c_char_p(b), _u8p)
+
+
 class StarkProof:
-    """Serialized winterfell::StarkProof (to_bytes layout: DESIGN.md "Proof format")."""
+    """Serialized winterfell::StarkProof (to_bytes layout: DESIGN.md "Proof format").
+    StarkProof.from_bytes parses and validates the structure (xfg_proof_parse); the parsed header is
+    exposed as attributes (trace_length, options, num_unique_queries, pow_nonce, ...)."""
 
     def __init__(self, data: bytes):
         self._data = bytes(data)
+        self._info = None
+
+    @classmethod
+    def from_bytes(cls, data: bytes):
+        p = cls(data)
+        p._parse()
+        return p
+
+    def _parse(self):
+        if self._info is None:
+            info, err = _ProofInfo(), C.create_string_buffer(256)
+            st = _lib.xfg_proof_parse(_bytes_ptr(self._data), len(self._data), C.byref(info), err, 256)
+            if st:
+                raise XfgStarkError(st, err.value.decode())
+            self._info = info
+        return self._info
 
     def to_bytes(self) -> bytes:
         return self._data
+
+    @property
+    def trace_length(self):
+        return self._parse().trace_length
+
+    @property
+    def options(self):
+        o = self._parse().options
+        return ProofOptions(o.num_queries, o.blowup_factor, o.grinding_factor, o.field_extension,
+                            o.fri_folding_factor, o.fri_remainder_max_degree)
+
+    @property
+    def num_unique_queries(self):
+        return self._parse().num_unique_queries
+
+    @property
+    def num_fri_layers(self):
+        return self._parse().num_fri_layers
+
+    @property
+    def pow_nonce(self):
+        return self._parse().pow_nonce
+
+    @property
+    def trace_root(self):
+        return bytes(self._parse().trace_root)
+
+    @property
+    def constraint_root(self):
+        return bytes(self._parse().constraint_root)
+
+    @property
+    def ood_frame(self):
+        """([T_c(z)], [T_c(z g)], H(z))"""
+        i = self._parse()
+        return list(i.ood_trace[0::2]), list(i.ood_trace[1::2]), i.ood_composition
 
     def __len__(self):
         return len(self._data)
 
     def __eq__(self, other):
         return isinstance(other, StarkProof) and other._data == self._data
+
+
+def _air_struct(air):
+    pub, nullifier, commitment = air
+    a = _AirConsts()
+    a.pub_inputs = (C.c_uint64 * 12)(*pub)
+    a.nullifier = nullifier
+    a.commitment = commitment
+    return a
+
+
+class XfgBurnMintVerifier:
+    """Mirror of the reference XfgBurnMintVerifier (src/burn_mint_verifier.rs:78-316) over
+    xfg_verify. The statement of a proof is its AIR constants `air` = (public inputs[12], nullifier,
+    commitment), as returned by air_consts(); acceptable options default to the reference's
+    ProofOptions::new(42, 8, 4, None, 8, 31) (:95-110)."""
+
+    def __init__(self, security_parameter=128, proof_options=None):
+        self.security_parameter = security_parameter
+        self.proof_options = proof_options or ProofOptions.reference()
+
+    @classmethod
+    def with_options(cls, security_parameter, proof_options):
+        return cls(security_parameter, proof_options)
+
+    def verify_with_details(self, proof, air):
+        """-> (accepted, error text or None, proof size)"""
+        data = proof.to_bytes() if isinstance(proof, StarkProof) else bytes(proof)
+        a, o, err = _air_struct(air), self.proof_options._c(), C.create_string_buffer(256)
+        st = _lib.xfg_verify(_bytes_ptr(data), len(data), C.byref(a), C.byref(o), err, 256)
+        if st not in (0, 10):
+            raise XfgStarkError(st, STATUS.get(st))
+        return st == 0, (err.value.decode() or None), len(data)
+
+    def verify_with_public_inputs(self, proof, air):
+        return self.verify_with_details(proof, air)[0]
+
+    def verify_burn_mint(self, proof, burn_amount, mint_amount, tx_prefix_hash, recipient_address, secret,
+                         network_id=1, target_chain_id=42161, commitment_version=1):
+        """statement rebuilt from the prover's inputs (the full 32-byte tx hash limbs included: the
+        reference's zeroed limbs at :146-150 would reject every honest proof)"""
+        air = air_consts(burn_amount, mint_amount, tx_prefix_hash, recipient_address, secret, network_id,
+                         target_chain_id, commitment_version)
+        return self.verify_with_public_inputs(proof, air)
+
+    def batch_verify(self, proofs_and_airs, threads=0):
+        """BatchBurnMintVerifier::verify_batch: list of (proof, air) -> list of bool (host threads)"""
+        k = len(proofs_and_airs)
+        if k == 0:
+            return []
+        datas = [(p.to_bytes() if isinstance(p, StarkProof) else bytes(p)) for p, _ in proofs_and_airs]
+        ptrs = (_u8p * k)(*[_bytes_ptr(d) for d in datas])
+        lens = (C.c_size_t * k)(*[len(d) for d in datas])
+        airs = (_AirConsts * k)(*[_air_struct(a) for _, a in proofs_and_airs])
+        res = (C.c_int * k)()
+        o = self.proof_options._c()
+        st = _lib.xfg_verify_batch(k, ptrs, lens, airs, C.byref(o), res, threads)
+        if st:
+            raise XfgStarkError(st, STATUS.get(st))
+        return [r == 0 for r in res]
+
+    def verify_all(self, proofs_and_airs, threads=0):
+        return all(self.batch_verify(proofs_and_airs, threads))
+
+
+def blake3(data: bytes) -> bytes:
+    """the library's host BLAKE3 (any length)"""
+    out = (C.c_uint8 * 32)()
+    _lib.xfg_selftest_blake3(_bytes_ptr(bytes(data)), len(data), out)
+    return bytes(out)
 
 
 def burn_inputs(burn_amount, mint_amount, tx_prefix_hash, recipient_address, secret, network_id=1,
