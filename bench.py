@@ -121,6 +121,17 @@ def pipelined_steps(submit_fn, collect_fn, batches, rank, world, per_rank, devic
     return gather_proofs(collect_fn(pending), rank, world, per_rank, device, dist)
 
 
+def pmc_traffic(per, n, blowup):
+    """HBM bytes per trace-LDE launch set from the committed PMC pass (profiles/rNN/lde_pmc.json,
+    made by scripts/profile_round.sh: FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 --pmc runs)"""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "lde_pmc.json")), reverse=True):
+        d = json.load(open(f))
+        if (d.get("count"), d.get("n"), d.get("blowup")) == (per, n, blowup):
+            return d["traffic_bytes"], os.path.relpath(f, ROOT)
+    return None, None
+
+
 def cpu_baseline(seconds=10.0):
     """oracle C restatement, single thread, faithful mode (per-row Keccak like the reference)"""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -221,6 +232,7 @@ def main():
     lde_ms = prover.bench_lde(per, n, BLOWUP, 10)
     lde_bytes = 8 * WIDTH * (n + n * BLOWUP) * per
     achieved = lde_bytes / (lde_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(per, n, BLOWUP)
     prover.set_timing(True)
     prover_stage = {}
     if rank == 0:
@@ -251,7 +263,8 @@ def main():
                 "submission": "pipelined, depth 2 (xfg_prove_batch_submit / xfg_batch_wait)",
             },
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
+                         "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": "trace LDE (ntt_pass_a<8,false> + ntt_pass_b<8,false>), 7 columns x "
                                    f"{per} proofs, {lde_ms:.3f} ms/launch-set, {lde_bytes} algorithmic B"},
             "stage_ms_one_batch": prover_stage,
