@@ -240,6 +240,29 @@ def test_other_options_match_oracle_and_verify(prover, n, kw):
     assert xfgstark.XfgBurnMintVerifier(proof_options=o).verify_burn_mint(proof, **kws)
 
 
+def test_generate_from_data_package_matches_golden(prover, tmp_path):
+    """CLI `generate` path: data package JSON -> MI355X proof -> proof package JSON; the proof bytes
+    equal the committed oracle fixture for the reference package (n = 64, blowup 8)"""
+    import test_package as TP
+    from xfgstark import package as K
+    with_blowup(prover, 8)
+    src, dst = tmp_path / "pkg.json", tmp_path / "proof.json"
+    src.write_text(json.dumps(TP._package()))
+    K.generate_proof(prover, str(src), str(dst), trace_length=64, created_at="2025-08-30T06:00:00+00:00")
+    data, pub, meta = K.load_proof_package(str(dst))
+    case = [c for c in json.load(open(os.path.join(GOLD, "proofs.json"))) if c["name"] == "pkg_n64_b8"][0]
+    assert data.hex() == case["proof_hex"]
+    # batch generate: invalid packages are reported, valid ones proven in one batch
+    pk = [K.StarkProofDataPackage(TP._package()),
+          K.StarkProofDataPackage(TP._package(**{"burn_transaction.burn_amount_xfg": "1.0"})),
+          K.StarkProofDataPackage(TP._package(**{"burn_transaction.transaction_hash": "00"})),
+          K.StarkProofDataPackage(TP._package())]
+    res = K.generate_proofs(prover, pk, trace_length=64)
+    assert res[1][0] is None and not res[1][1].is_valid
+    assert res[2][0] is None and isinstance(res[2][1], K.PackageError)
+    assert bytes(res[0][0]["proof_data"]) == bytes(res[3][0]["proof_data"]) == data
+
+
 def test_rejects_options_the_reference_rejects(prover):
     import xfgstark
     kw = synthetic.burn_inputs(3)
