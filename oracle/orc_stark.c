@@ -311,7 +311,7 @@ static int check_options(uint64_t n, const orc_options* o) {
     if (!is_pow2(o->blowup) || o->blowup < CE_BLOWUP || o->blowup > 128) return -1;
     if (o->num_queries < 1 || o->num_queries > 255) return -1;
     if (o->grinding > 32) return -1;
-    if (o->field_extension != 1) return -1; /* base field only in this restatement */
+    if (o->field_extension != 1 && o->field_extension != 2) return -1; /* None or Quadratic */
     if (o->fri_folding != 2 && o->fri_folding != 4 && o->fri_folding != 8 && o->fri_folding != 16) return -1;
     if (o->fri_rem_max_deg > 255 || !is_pow2((uint64_t)o->fri_rem_max_deg + 1)) return -1;
     if ((uint64_t)o->num_queries >= n * o->blowup) return -1;
@@ -382,9 +382,13 @@ static void fold_positions(const uint64_t* in, uint64_t k, uint64_t target, uint
 }
 
 /* ============================================================ prover */
+static int orc_prove_quad(const orc_air* air, const uint64_t* trace, uint64_t n, const orc_options* opt, int faithful,
+                          uint8_t* out, size_t* out_len, orc_debug* dbg);
+static int orc_verify_quad(const orc_air* air, const uint8_t* proof, size_t len, const orc_options* opt);
 int orc_prove(const orc_air* air, const uint64_t* trace, uint64_t n, const orc_options* opt, int faithful,
               uint8_t* out, size_t* out_len, orc_debug* dbg) {
     if (check_options(n, opt)) return ORC_PROVER_ERROR;
+    if (opt->field_extension == 2) return orc_prove_quad(air, trace, n, opt, faithful, out, out_len, dbg);
     const uint64_t beta = opt->blowup, N = n * beta, nce = CE_BLOWUP * n, f = opt->fri_folding;
     const uint64_t g = orc_root(ilog2u(n));
     int status = ORC_OK;
@@ -725,6 +729,7 @@ static int batch_root(const uint8_t* paths, size_t plen, const uint64_t* idx, ui
 }
 
 int orc_verify(const orc_air* air, const uint8_t* proof, size_t len, const orc_options* opt) {
+    if (opt->field_extension == 2) return orc_verify_quad(air, proof, len, opt);
     brd r = {proof, len, 0, 0};
     /* context */
     uint64_t width = rd_u(&r, 1), naux = rd_u(&r, 1), logn = rd_u(&r, 1), meta = rd_u(&r, 2);
@@ -882,6 +887,518 @@ int orc_verify(const orc_air* air, const uint8_t* proof, size_t len, const orc_o
         const uint64_t wD = orc_root(ilog2u(D));
         for (uint64_t i = 0; ok && i < ck; i++)
             if (horner(remc, rl, orc_mul(ORC_GEN, orc_pow(wD, cp_pos[i]))) != ev[i]) ok = 0;
+    }
+    free(ld);
+    return ok ? ORC_OK : ORC_VERIFY_FAILED;
+}
+
+/* ============================================================ quadratic extension (RECALLED)
+ * FieldExtension::Quadratic of winter-math f64: E = F[phi]/(phi^2 - phi + 2), elements a + b phi
+ * serialised as (a, b) canonical LE u64s. With it the trace and its commitment stay in the base
+ * field; the composition coefficients, the OOD point z, the DEEP coefficients and the FRI
+ * alphas are drawn as E (16 digest bytes -> two elements, retry if either is >= p); constraint
+ * evaluations, composition polynomial, OOD frame, DEEP polynomial, FRI layers and remainder are
+ * E-valued. Base-field linear maps (NTTs, the iDFT of a FRI fold) act per coordinate. */
+typedef struct { uint64_t a, b; } fq;
+static fq fq_make(uint64_t a, uint64_t b) { fq r; r.a = a; r.b = b; return r; }
+static fq fq_add(fq x, fq y) { return fq_make(orc_add(x.a, y.a), orc_add(x.b, y.b)); }
+static fq fq_sub(fq x, fq y) { return fq_make(orc_sub(x.a, y.a), orc_sub(x.b, y.b)); }
+static fq fq_mulb(fq x, uint64_t s) { return fq_make(orc_mul(x.a, s), orc_mul(x.b, s)); }
+static fq fq_mul(fq x, fq y) {
+    /* (a0 + a1 phi)(b0 + b1 phi) = a0 b0 - 2 a1 b1 + (a0 b1 + a1 b0 + a1 b1) phi */
+    uint64_t a0b0 = orc_mul(x.a, y.a), a1b1 = orc_mul(x.b, y.b);
+    uint64_t cross = orc_add(orc_add(orc_mul(x.a, y.b), orc_mul(x.b, y.a)), a1b1);
+    return fq_make(orc_sub(a0b0, orc_add(a1b1, a1b1)), cross);
+}
+static fq fq_inv(fq x) {
+    /* x^-1 = frob(x) / (x frob(x)), frob(a + b phi) = (a + b) - b phi, the norm is in F */
+    fq f = fq_make(orc_add(x.a, x.b), orc_sub(0, x.b));
+    fq nrm = fq_mul(x, f);
+    return fq_mulb(f, orc_inv(nrm.a));
+}
+static int fq_eq(fq x, fq y) { return x.a == y.a && x.b == y.b; }
+static int fq_is_zero(fq x) { return x.a == 0 && x.b == 0; }
+static int coin_draw_fq(coin_t* c, fq* out) {
+    for (int i = 0; i < 1000; i++) {
+        uint8_t h[32];
+        coin_next(c, h);
+        uint64_t a = get_le64(h), b = get_le64(h + 8);
+        if (a < ORC_P && b < ORC_P) { *out = fq_make(a, b); return 0; }
+    }
+    return -1;
+}
+static void hash_fq(const fq* e, size_t cnt, uint8_t out[32]) {
+    uint8_t* buf = (uint8_t*)malloc(cnt * 16 + 1);
+    for (size_t i = 0; i < cnt; i++) { put_le64(buf + 16 * i, e[i].a); put_le64(buf + 16 * i + 8, e[i].b); }
+    orc_blake3(buf, cnt * 16, out);
+    free(buf);
+}
+static void bb_fq(bbuf* w, fq v) { bb_u64(w, v.a); bb_u64(w, v.b); }
+static fq horner_bq(const uint64_t* c, uint64_t n, fq x) { /* base coefficients at an E point */
+    fq r = fq_make(0, 0);
+    for (uint64_t j = n; j-- > 0;) r = fq_add(fq_mul(r, x), fq_make(c[j], 0));
+    return r;
+}
+static fq horner_q(const fq* c, uint64_t n, fq x) {
+    fq r = fq_make(0, 0);
+    for (uint64_t j = n; j-- > 0;) r = fq_add(fq_mul(r, x), c[j]);
+    return r;
+}
+static void syn_div_q(fq* a, uint64_t n, fq b) {
+    fq c = fq_make(0, 0);
+    for (uint64_t j = n; j-- > 0;) {
+        fq v = fq_add(a[j], fq_mul(b, c));
+        a[j] = c;
+        c = v;
+    }
+}
+/* per-coordinate NTT helpers over fq arrays */
+static void split_q(const fq* v, uint64_t n, uint64_t* x, uint64_t* y) {
+    for (uint64_t i = 0; i < n; i++) { x[i] = v[i].a; y[i] = v[i].b; }
+}
+static void join_q(const uint64_t* x, const uint64_t* y, uint64_t n, fq* v) {
+    for (uint64_t i = 0; i < n; i++) v[i] = fq_make(x[i], y[i]);
+}
+static void interpolate_q(fq* v, uint64_t n, uint64_t offset) {
+    uint64_t* x = (uint64_t*)malloc(n * 8);
+    uint64_t* y = (uint64_t*)malloc(n * 8);
+    split_q(v, n, x, y);
+    orc_interpolate(x, n, offset);
+    orc_interpolate(y, n, offset);
+    join_q(x, y, n, v);
+    free(x); free(y);
+}
+static void lde_q(const fq* c, uint64_t n, uint64_t blowup, fq* out) {
+    uint64_t N = n * blowup;
+    uint64_t* x = (uint64_t*)malloc(n * 8);
+    uint64_t* y = (uint64_t*)malloc(n * 8);
+    uint64_t* X = (uint64_t*)malloc(N * 8);
+    uint64_t* Y = (uint64_t*)malloc(N * 8);
+    split_q(c, n, x, y);
+    orc_evaluate_lde(x, n, blowup, ORC_GEN, X);
+    orc_evaluate_lde(y, n, blowup, ORC_GEN, Y);
+    join_q(X, Y, N, out);
+    free(x); free(y); free(X); free(Y);
+}
+static fq fri_fold_row_q(const fq* v, uint32_t f, uint64_t x, fq alpha) {
+    uint64_t zinv = orc_inv(orc_root(ilog2u(f))), finv = orc_inv(f);
+    fq c[16];
+    for (uint32_t j = 0; j < f; j++) {
+        fq s = fq_make(0, 0);
+        uint64_t wj = orc_pow(zinv, j), w = 1;
+        for (uint32_t k = 0; k < f; k++) { s = fq_add(s, fq_mulb(v[k], w)); w = orc_mul(w, wj); }
+        c[j] = fq_mulb(s, finv);
+    }
+    return horner_q(c, f, fq_mulb(alpha, orc_inv(x)));
+}
+static void air_transition_q(const orc_air* air, const fq cur[7], const fq nxt[7], fq r[7]) {
+    uint64_t large = orc_mul(STANDARD_BURN, 1000);
+    r[0] = fq_mul(fq_sub(cur[0], fq_make(STANDARD_BURN, 0)), fq_sub(cur[0], fq_make(large, 0)));
+    r[1] = fq_sub(cur[1], cur[0]);
+    r[2] = fq_sub(cur[2], fq_make((uint32_t)air->pub[PI_TXN], 0));
+    r[3] = fq_sub(cur[3], fq_make((uint32_t)air->pub[PI_RH], 0));
+    fq d = fq_sub(nxt[4], cur[4]);
+    r[4] = fq_mul(d, fq_sub(d, fq_make(1, 0)));
+    r[5] = fq_sub(cur[5], fq_make(air->nullifier, 0));
+    r[6] = fq_sub(cur[6], fq_make(air->commitment, 0));
+}
+
+static int orc_prove_quad(const orc_air* air, const uint64_t* trace, uint64_t n, const orc_options* opt, int faithful,
+                          uint8_t* out, size_t* out_len, orc_debug* dbg) {
+    const uint64_t beta = opt->blowup, N = n * beta, nce = CE_BLOWUP * n, f = opt->fri_folding;
+    const uint64_t g = orc_root(ilog2u(n));
+    int status = ORC_OK;
+    uint64_t seed_e[20];
+    size_t ne = context_elements(n, opt, seed_e);
+    memcpy(seed_e + ne, air->pub, 12 * sizeof(uint64_t));
+    coin_t coin;
+    coin_init(&coin, seed_e, ne + 12);
+    bbuf commitments = {0};
+
+    /* 1. trace (base field, as without extension) */
+    uint64_t* coef = (uint64_t*)malloc(W * n * sizeof(uint64_t));
+    uint64_t* lde = (uint64_t*)malloc(W * N * sizeof(uint64_t));
+    for (int c = 0; c < W; c++) {
+        memcpy(coef + c * n, trace + c * n, n * sizeof(uint64_t));
+        orc_interpolate(coef + c * n, n, 1);
+        orc_evaluate_lde(coef + c * n, n, beta, ORC_GEN, lde + c * N);
+    }
+    dg* leaves = (dg*)malloc(N * sizeof(dg));
+    for (uint64_t k = 0; k < N; k++) {
+        uint64_t row[W];
+        for (int c = 0; c < W; c++) row[c] = lde[c * N + k];
+        hash_elems(row, W, leaves[k]);
+    }
+    mtree ttree;
+    mtree_build(&ttree, leaves, N);
+    bb_put(&commitments, ttree.nodes[1], 32);
+    coin_reseed(&coin, ttree.nodes[1]);
+
+    /* 2. composition coefficients in E */
+    fq alpha[W], bcoef[NUM_ASSERT];
+    for (int i = 0; i < W; i++) if (coin_draw_fq(&coin, &alpha[i])) status = ORC_PROVER_ERROR;
+    for (int i = 0; i < NUM_ASSERT; i++) if (coin_draw_fq(&coin, &bcoef[i])) status = ORC_PROVER_ERROR;
+
+    /* 3. constraint evaluations (E) on the CE coset */
+    uint64_t acol[NUM_ASSERT], astep[NUM_ASSERT], aval[NUM_ASSERT];
+    air_assertions(air, n, acol, astep, aval);
+    fq* ce = (fq*)malloc(nce * sizeof(fq));
+    const uint64_t wce = orc_root(ilog2u(nce)), g_last = orc_pow(g, n - 1);
+    uint64_t x = ORC_GEN;
+    for (uint64_t i = 0; i < nce; i++, x = orc_mul(x, wce)) {
+        uint64_t k = i * (beta / CE_BLOWUP), kn = (k + beta) % N, cur[W], nxt[W], r[W];
+        for (int c = 0; c < W; c++) { cur[c] = lde[c * N + k]; nxt[c] = lde[c * N + kn]; }
+        air_transition(air, cur, nxt, faithful, r);
+        fq t = fq_make(0, 0);
+        for (int c = 0; c < W; c++) t = fq_add(t, fq_mulb(alpha[c], r[c]));
+        uint64_t zt = orc_mul(orc_sub(orc_pow(x, n), 1), orc_inv(orc_sub(x, g_last)));
+        fq acc = fq_mulb(t, orc_inv(zt));
+        fq b0 = fq_make(0, 0), b1 = fq_make(0, 0);
+        for (int a = 0; a < NUM_ASSERT; a++) {
+            fq term = fq_mulb(bcoef[a], orc_sub(cur[acol[a]], aval[a]));
+            if (astep[a] == 0) b0 = fq_add(b0, term); else b1 = fq_add(b1, term);
+        }
+        acc = fq_add(acc, fq_mulb(b0, orc_inv(orc_sub(x, 1))));
+        acc = fq_add(acc, fq_mulb(b1, orc_inv(orc_sub(x, g_last))));
+        ce[i] = acc;
+    }
+
+    /* 4. composition polynomial (E), LDE per coordinate, leaves = hash of one E element */
+    interpolate_q(ce, nce, ORC_GEN);
+    fq* hcoef = (fq*)malloc(n * sizeof(fq));
+    memcpy(hcoef, ce, n * sizeof(fq));
+    fq* hlde = (fq*)malloc(N * sizeof(fq));
+    lde_q(hcoef, n, beta, hlde);
+    for (uint64_t k = 0; k < N; k++) hash_fq(&hlde[k], 1, leaves[k]);
+    mtree htree;
+    mtree_build(&htree, leaves, N);
+    bb_put(&commitments, htree.nodes[1], 32);
+    coin_reseed(&coin, htree.nodes[1]);
+
+    /* 5. OOD point z in E, frame, DEEP coefficients */
+    fq z;
+    if (coin_draw_fq(&coin, &z)) status = ORC_PROVER_ERROR;
+    fq zg = fq_mulb(z, g), ood[2 * W], hz;
+    for (int c = 0; c < W; c++) {
+        ood[2 * c] = horner_bq(coef + c * n, n, z);
+        ood[2 * c + 1] = horner_bq(coef + c * n, n, zg);
+    }
+    hz = horner_q(hcoef, n, z);
+    uint8_t dtmp[32];
+    hash_fq(ood, 2 * W, dtmp);
+    coin_reseed(&coin, dtmp);
+    hash_fq(&hz, 1, dtmp);
+    coin_reseed(&coin, dtmp);
+    fq dc[W], gam;
+    for (int c = 0; c < W; c++) if (coin_draw_fq(&coin, &dc[c])) status = ORC_PROVER_ERROR;
+    if (coin_draw_fq(&coin, &gam)) status = ORC_PROVER_ERROR;
+    if (dbg) {
+        dbg->z = z.a;
+        for (int c = 0; c < 2 * W; c++) dbg->ood[c] = ood[c].a;
+        dbg->ood[14] = hz.a;
+    }
+
+    /* 6. DEEP composition polynomial (E coefficients) */
+    fq* t1 = (fq*)calloc(n, sizeof(fq));
+    fq* t2 = (fq*)calloc(n, sizeof(fq));
+    for (int c = 0; c < W; c++) {
+        for (uint64_t j = 0; j < n; j++) {
+            fq v = fq_mulb(dc[c], coef[c * n + j]);
+            t1[j] = fq_add(t1[j], v);
+            t2[j] = fq_add(t2[j], v);
+        }
+        t1[0] = fq_sub(t1[0], fq_mul(dc[c], ood[2 * c]));
+        t2[0] = fq_sub(t2[0], fq_mul(dc[c], ood[2 * c + 1]));
+    }
+    syn_div_q(t1, n, z);
+    syn_div_q(t2, n, zg);
+    for (uint64_t j = 0; j < n; j++) t1[j] = fq_add(t1[j], t2[j]);
+    hcoef[0] = fq_sub(hcoef[0], hz);
+    syn_div_q(hcoef, n, z);
+    for (uint64_t j = 0; j < n; j++) t1[j] = fq_add(t1[j], fq_mul(gam, hcoef[j]));
+    uint64_t deg = 0;
+    for (uint64_t j = 0; j < n; j++) if (!fq_is_zero(t1[j])) deg = j;
+    if (deg != n - 2) status = ORC_PROVER_ERROR;
+
+    /* 7. FRI over E values */
+    uint32_t nl = num_fri_layers(N, opt);
+    fq** layer = (fq**)malloc((nl + 1) * sizeof(fq*));
+    mtree* ftree = (mtree*)malloc((nl ? nl : 1) * sizeof(mtree));
+    layer[0] = (fq*)malloc(N * sizeof(fq));
+    lde_q(t1, n, beta, layer[0]);
+    uint64_t D = N;
+    for (uint32_t l = 0; l < nl; l++) {
+        uint64_t rows = D / f;
+        for (uint64_t i = 0; i < rows; i++) {
+            fq v[16];
+            for (uint64_t k = 0; k < f; k++) v[k] = layer[l][i + k * rows];
+            hash_fq(v, f, leaves[i]);
+        }
+        mtree_build(&ftree[l], leaves, rows);
+        bb_put(&commitments, ftree[l].nodes[1], 32);
+        coin_reseed(&coin, ftree[l].nodes[1]);
+        fq a;
+        if (coin_draw_fq(&coin, &a)) status = ORC_PROVER_ERROR;
+        layer[l + 1] = (fq*)malloc(rows * sizeof(fq));
+        const uint64_t wD = orc_root(ilog2u(D));
+        uint64_t xi = ORC_GEN;
+        for (uint64_t i = 0; i < rows; i++, xi = orc_mul(xi, wD)) {
+            fq v[16];
+            for (uint64_t k = 0; k < f; k++) v[k] = layer[l][i + k * rows];
+            layer[l + 1][i] = fri_fold_row_q(v, (uint32_t)f, xi, a);
+        }
+        D = rows;
+    }
+    fq* rem = (fq*)malloc(D * sizeof(fq));
+    memcpy(rem, layer[nl], D * sizeof(fq));
+    interpolate_q(rem, D, ORC_GEN);
+    uint64_t rem_len = D / beta;
+    hash_fq(rem, rem_len, dtmp);
+    bb_put(&commitments, dtmp, 32);
+    coin_reseed(&coin, dtmp);
+
+    /* 8. grinding + query positions */
+    uint64_t nonce = 1;
+    for (;; nonce++) {
+        uint8_t h[32];
+        merge_int(coin.seed, nonce, h);
+        if (tz64(get_le64(h)) >= opt->grinding) break;
+    }
+    coin_reseed_int(&coin, nonce);
+    uint64_t q = opt->num_queries, pos[256];
+    for (uint64_t i = 0; i < q; i++) {
+        uint8_t h[32];
+        coin_next(&coin, h);
+        pos[i] = get_le64(h) & (N - 1);
+    }
+    qsort(pos, q, sizeof(uint64_t), cmp_u64);
+    uint64_t nu = 0;
+    for (uint64_t i = 0; i < q; i++) if (nu == 0 || pos[nu - 1] != pos[i]) pos[nu++] = pos[i];
+    if (dbg) {
+        dbg->pow_nonce = nonce;
+        dbg->num_unique_queries = (uint32_t)nu;
+        for (uint64_t i = 0; i < nu; i++) dbg->positions[i] = pos[i];
+        dbg->num_fri_layers = nl;
+    }
+
+    /* 9. StarkProof::to_bytes with 16-byte E elements */
+    bbuf w = {0}, tmp = {0};
+    write_context(&w, n, opt);
+    bb_u8(&w, (uint8_t)nu);
+    bb_u16(&w, (uint16_t)commitments.n);
+    bb_put(&w, commitments.b, commitments.n);
+    bb_u8(&w, 1);
+    bb_u32(&w, (uint32_t)(nu * W * 8));
+    for (uint64_t i = 0; i < nu; i++) for (int c = 0; c < W; c++) bb_u64(&w, lde[c * N + pos[i]]);
+    tmp.n = 0;
+    mtree_prove_serialize(&ttree, pos, nu, &tmp);
+    bb_u32(&w, (uint32_t)tmp.n);
+    bb_put(&w, tmp.b, tmp.n);
+    bb_u32(&w, (uint32_t)(nu * 16));
+    for (uint64_t i = 0; i < nu; i++) bb_fq(&w, hlde[pos[i]]);
+    tmp.n = 0;
+    mtree_prove_serialize(&htree, pos, nu, &tmp);
+    bb_u32(&w, (uint32_t)tmp.n);
+    bb_put(&w, tmp.b, tmp.n);
+    bb_u16(&w, (uint16_t)(1 + 2 * W * 16));
+    bb_u8(&w, 2);
+    for (int c = 0; c < 2 * W; c++) bb_fq(&w, ood[c]);
+    bb_u16(&w, 16);
+    bb_fq(&w, hz);
+    bb_u8(&w, (uint8_t)nl);
+    uint64_t fpos[256], fk = nu;
+    memcpy(fpos, pos, nu * sizeof(uint64_t));
+    D = N;
+    for (uint32_t l = 0; l < nl; l++) {
+        uint64_t rows = D / f, np[256], nk;
+        fold_positions(fpos, fk, rows, np, &nk);
+        bb_u32(&w, (uint32_t)(nk * f * 16));
+        for (uint64_t i = 0; i < nk; i++) for (uint64_t k = 0; k < f; k++) bb_fq(&w, layer[l][np[i] + k * rows]);
+        tmp.n = 0;
+        mtree_prove_serialize(&ftree[l], np, nk, &tmp);
+        bb_u32(&w, (uint32_t)tmp.n);
+        bb_put(&w, tmp.b, tmp.n);
+        memcpy(fpos, np, nk * sizeof(uint64_t));
+        fk = nk;
+        D = rows;
+    }
+    bb_u16(&w, (uint16_t)(rem_len * 16));
+    for (uint64_t i = 0; i < rem_len; i++) bb_fq(&w, rem[i]);
+    bb_u8(&w, 0);
+    bb_u64(&w, nonce);
+
+    if (status == ORC_OK) {
+        if (!out) *out_len = w.n;
+        else if (*out_len < w.n) { *out_len = w.n; status = ORC_BUFFER_TOO_SMALL; }
+        else { memcpy(out, w.b, w.n); *out_len = w.n; }
+    }
+    free(w.b); free(tmp.b); free(commitments.b);
+    for (uint32_t l = 0; l <= nl; l++) free(layer[l]);
+    for (uint32_t l = 0; l < nl; l++) mtree_free(&ftree[l]);
+    free(layer); free(ftree); free(rem);
+    free(t1); free(t2); free(hcoef); free(hlde); free(ce); free(leaves); free(coef); free(lde);
+    mtree_free(&ttree); mtree_free(&htree);
+    return status;
+}
+
+static fq rd_fq(const uint8_t* p) { return fq_make(get_le64(p), get_le64(p + 8)); }
+static int orc_verify_quad(const orc_air* air, const uint8_t* proof, size_t len, const orc_options* opt) {
+    brd r = {proof, len, 0, 0};
+    uint64_t width = rd_u(&r, 1), naux = rd_u(&r, 1), logn = rd_u(&r, 1), meta = rd_u(&r, 2);
+    rd(&r, meta);
+    uint64_t mlen = rd_u(&r, 1), modulus = rd_u(&r, 8);
+    orc_options o;
+    o.num_queries = (uint32_t)rd_u(&r, 1); o.blowup = (uint32_t)rd_u(&r, 1); o.grinding = (uint32_t)rd_u(&r, 1);
+    o.field_extension = (uint32_t)rd_u(&r, 1); o.fri_folding = (uint32_t)rd_u(&r, 1); o.fri_rem_max_deg = (uint32_t)rd_u(&r, 1);
+    if (r.err || width != W || naux != 0 || mlen != 8 || modulus != ORC_P || logn > 26) return ORC_VERIFY_FAILED;
+    if (memcmp(&o, opt, sizeof o)) return ORC_VERIFY_FAILED;
+    uint64_t n = 1ULL << logn;
+    if (check_options(n, &o)) return ORC_VERIFY_FAILED;
+    const uint64_t beta = o.blowup, N = n * beta, f = o.fri_folding, depth = ilog2u(N);
+    const uint64_t g = orc_root((unsigned)logn);
+    uint32_t nl = num_fri_layers(N, &o);
+    uint64_t nu = rd_u(&r, 1);
+    uint64_t clen = rd_u(&r, 2);
+    const uint8_t* com = rd(&r, clen);
+    if (r.err || clen != 32ULL * (3 + nl) || nu == 0) return ORC_VERIFY_FAILED;
+    if (rd_u(&r, 1) != 1) return ORC_VERIFY_FAILED;
+    uint64_t tvl = rd_u(&r, 4); const uint8_t* tv = rd(&r, tvl);
+    uint64_t tpl = rd_u(&r, 4); const uint8_t* tp = rd(&r, tpl);
+    uint64_t cvl = rd_u(&r, 4); const uint8_t* cv = rd(&r, cvl);
+    uint64_t cpl = rd_u(&r, 4); const uint8_t* cp = rd(&r, cpl);
+    uint64_t osl = rd_u(&r, 2); const uint8_t* os = rd(&r, osl);
+    uint64_t oel = rd_u(&r, 2); const uint8_t* oe = rd(&r, oel);
+    if (r.err || tvl != nu * W * 8 || cvl != nu * 16 || osl != 1 + 2 * W * 16 || oel != 16 || os[0] != 2)
+        return ORC_VERIFY_FAILED;
+    uint64_t nfl = rd_u(&r, 1);
+    if (nfl != nl) return ORC_VERIFY_FAILED;
+    const uint8_t *fv[16], *fp[16];
+    uint64_t fvl[16], fpl[16];
+    for (uint32_t l = 0; l < nl; l++) {
+        fvl[l] = rd_u(&r, 4); fv[l] = rd(&r, fvl[l]);
+        fpl[l] = rd_u(&r, 4); fp[l] = rd(&r, fpl[l]);
+    }
+    uint64_t rml = rd_u(&r, 2); const uint8_t* rm = rd(&r, rml);
+    uint64_t parts = rd_u(&r, 1);
+    uint64_t nonce = rd_u(&r, 8);
+    if (r.err || r.off != len || parts != 0) return ORC_VERIFY_FAILED;
+
+    uint64_t seed_e[20];
+    size_t ne = context_elements(n, &o, seed_e);
+    memcpy(seed_e + ne, air->pub, 12 * sizeof(uint64_t));
+    coin_t coin;
+    coin_init(&coin, seed_e, ne + 12);
+    coin_reseed(&coin, com);
+    fq alpha[W], bcoef[NUM_ASSERT], z, dc[W], gam;
+    for (int i = 0; i < W; i++) if (coin_draw_fq(&coin, &alpha[i])) return ORC_VERIFY_FAILED;
+    for (int i = 0; i < NUM_ASSERT; i++) if (coin_draw_fq(&coin, &bcoef[i])) return ORC_VERIFY_FAILED;
+    coin_reseed(&coin, com + 32);
+    if (coin_draw_fq(&coin, &z)) return ORC_VERIFY_FAILED;
+    fq ood[2 * W], hz = rd_fq(oe), zg = fq_mulb(z, g);
+    for (int c = 0; c < 2 * W; c++) ood[c] = rd_fq(os + 1 + 16 * c);
+    {
+        fq cur[W], nxt[W], rr[W];
+        uint64_t acol[NUM_ASSERT], astep[NUM_ASSERT], aval[NUM_ASSERT];
+        for (int c = 0; c < W; c++) { cur[c] = ood[2 * c]; nxt[c] = ood[2 * c + 1]; }
+        air_transition_q(air, cur, nxt, rr);
+        fq t = fq_make(0, 0);
+        for (int c = 0; c < W; c++) t = fq_add(t, fq_mul(alpha[c], rr[c]));
+        uint64_t g_last = orc_pow(g, n - 1);
+        fq zn = fq_make(1, 0);
+        { fq b = z; uint64_t e = n; while (e) { if (e & 1) zn = fq_mul(zn, b); b = fq_mul(b, b); e >>= 1; } }
+        fq e = fq_mul(fq_mul(t, fq_sub(z, fq_make(g_last, 0))), fq_inv(fq_sub(zn, fq_make(1, 0))));
+        air_assertions(air, n, acol, astep, aval);
+        fq b0 = fq_make(0, 0), b1 = fq_make(0, 0);
+        for (int a = 0; a < NUM_ASSERT; a++) {
+            fq term = fq_mul(bcoef[a], fq_sub(cur[acol[a]], fq_make(aval[a], 0)));
+            if (astep[a] == 0) b0 = fq_add(b0, term); else b1 = fq_add(b1, term);
+        }
+        e = fq_add(e, fq_mul(b0, fq_inv(fq_sub(z, fq_make(1, 0)))));
+        e = fq_add(e, fq_mul(b1, fq_inv(fq_sub(z, fq_make(g_last, 0)))));
+        if (!fq_eq(e, hz)) return ORC_VERIFY_FAILED;
+    }
+    uint8_t dtmp[32];
+    hash_fq(ood, 2 * W, dtmp);
+    coin_reseed(&coin, dtmp);
+    hash_fq(&hz, 1, dtmp);
+    coin_reseed(&coin, dtmp);
+    for (int c = 0; c < W; c++) if (coin_draw_fq(&coin, &dc[c])) return ORC_VERIFY_FAILED;
+    if (coin_draw_fq(&coin, &gam)) return ORC_VERIFY_FAILED;
+    fq falpha[16];
+    for (uint32_t l = 0; l <= nl; l++) {
+        coin_reseed(&coin, com + 64 + 32 * l);
+        fq a;
+        if (coin_draw_fq(&coin, &a)) return ORC_VERIFY_FAILED;
+        if (l < nl) falpha[l] = a;
+    }
+    {
+        uint8_t h[32];
+        merge_int(coin.seed, nonce, h);
+        if (tz64(get_le64(h)) < o.grinding) return ORC_VERIFY_FAILED;
+    }
+    coin_reseed_int(&coin, nonce);
+    uint64_t pos[256], q = o.num_queries;
+    for (uint64_t i = 0; i < q; i++) { uint8_t h[32]; coin_next(&coin, h); pos[i] = get_le64(h) & (N - 1); }
+    qsort(pos, q, sizeof(uint64_t), cmp_u64);
+    uint64_t u = 0;
+    for (uint64_t i = 0; i < q; i++) if (u == 0 || pos[u - 1] != pos[i]) pos[u++] = pos[i];
+    if (u != nu) return ORC_VERIFY_FAILED;
+
+    int ok = 1;
+    dg* ld = (dg*)malloc(256 * sizeof(dg));
+    uint8_t root[32];
+    for (uint64_t i = 0; i < nu; i++) orc_blake3(tv + i * W * 8, W * 8, ld[i]);
+    if (batch_root(tp, tpl, pos, nu, ld, depth, root) || memcmp(root, com, 32)) ok = 0;
+    for (uint64_t i = 0; i < nu; i++) orc_blake3(cv + i * 16, 16, ld[i]);
+    if (ok && (batch_root(cp, cpl, pos, nu, ld, depth, root) || memcmp(root, com + 32, 32))) ok = 0;
+    fq ev[256];
+    const uint64_t wN = orc_root((unsigned)depth);
+    for (uint64_t i = 0; i < nu && ok; i++) {
+        uint64_t xb = orc_mul(ORC_GEN, orc_pow(wN, pos[i]));
+        fq xq = fq_make(xb, 0), s1 = fq_make(0, 0), s2 = fq_make(0, 0);
+        for (int c = 0; c < W; c++) {
+            fq tx = fq_make(get_le64(tv + (i * W + c) * 8), 0);
+            s1 = fq_add(s1, fq_mul(dc[c], fq_sub(tx, ood[2 * c])));
+            s2 = fq_add(s2, fq_mul(dc[c], fq_sub(tx, ood[2 * c + 1])));
+        }
+        fq hx = rd_fq(cv + i * 16);
+        fq izx = fq_inv(fq_sub(xq, z));
+        ev[i] = fq_add(fq_mul(s1, izx), fq_mul(s2, fq_inv(fq_sub(xq, zg))));
+        ev[i] = fq_add(ev[i], fq_mul(fq_mul(gam, fq_sub(hx, hz)), izx));
+    }
+    uint64_t D = N, cp_pos[256], ck = nu;
+    memcpy(cp_pos, pos, nu * sizeof(uint64_t));
+    for (uint32_t l = 0; l < nl && ok; l++) {
+        uint64_t rows = D / f, np[256], nk;
+        fold_positions(cp_pos, ck, rows, np, &nk);
+        if (fvl[l] != nk * f * 16) { ok = 0; break; }
+        for (uint64_t i = 0; i < nk; i++) orc_blake3(fv[l] + i * f * 16, f * 16, ld[i]);
+        if (batch_root(fp[l], fpl[l], np, nk, ld, ilog2u(rows), root) || memcmp(root, com + 64 + 32 * l, 32)) { ok = 0; break; }
+        for (uint64_t i = 0; i < ck; i++) {
+            uint64_t ri = cp_pos[i] % rows, e = cp_pos[i] / rows, idx = 0;
+            while (np[idx] != ri) idx++;
+            if (!fq_eq(rd_fq(fv[l] + (idx * f + e) * 16), ev[i])) { ok = 0; break; }
+        }
+        const uint64_t wD = orc_root(ilog2u(D));
+        for (uint64_t i = 0; i < nk && ok; i++) {
+            fq v[16];
+            for (uint64_t k = 0; k < f; k++) v[k] = rd_fq(fv[l] + (i * f + k) * 16);
+            ev[i] = fri_fold_row_q(v, (uint32_t)f, orc_mul(ORC_GEN, orc_pow(wD, np[i])), falpha[l]);
+        }
+        memcpy(cp_pos, np, nk * sizeof(uint64_t));
+        ck = nk;
+        D = rows;
+    }
+    if (ok) {
+        uint64_t rl = rml / 16;
+        fq* remc = (fq*)malloc((rl + 1) * sizeof(fq));
+        if (rml % 16 || rl == 0 || rl != D / beta) ok = 0;
+        for (uint64_t i = 0; ok && i < rl; i++) remc[i] = rd_fq(rm + 16 * i);
+        if (ok) { hash_fq(remc, rl, dtmp); if (memcmp(dtmp, com + 64 + 32 * nl, 32)) ok = 0; }
+        const uint64_t wD = orc_root(ilog2u(D));
+        for (uint64_t i = 0; ok && i < ck; i++)
+            if (!fq_eq(horner_q(remc, rl, fq_make(orc_mul(ORC_GEN, orc_pow(wD, cp_pos[i])), 0)), ev[i])) ok = 0;
+        free(remc);
     }
     free(ld);
     return ok ? ORC_OK : ORC_VERIFY_FAILED;

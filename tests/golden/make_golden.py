@@ -68,29 +68,37 @@ def reference_kats():
     }
 
 
-CASES = [  # (name, input source, n, blowup)
+CASES = [  # (name, input source, n, blowup[, other ProofOptions])
     ("pkg_n64_b8", "package", 64, 8),
     ("pkg_n64_b4", "package", 64, 4),
     ("syn0_n1024_b4", 0, 1024, 4),   # config 1 shape (2^10 steps, blowup 4)
     ("syn1_n1024_b8", 1, 1024, 8),
     ("syn2_n4096_b8", 2, 4096, 8),
     ("syn0_n65536_b8", 0, 65536, 8),  # config 2 shape (2^16 steps, blowup 8)
+    # FieldExtension::Quadratic (config 5's field): 16-byte E elements after the trace commitment
+    ("pkg_n64_b8_quad", "package", 64, 8, {"field_extension": 2}),
+    ("syn3_n4096_b16_quad_q24", 3, 4096, 16, {"field_extension": 2, "num_queries": 24}),
+    ("syn4_n65536_b8_quad", 4, 65536, 8, {"field_extension": 2}),
 ]
 
 
 def proof_fixtures():
     out = []
-    for name, src, n, b in CASES:
+    for case in CASES:
+        name, src, n, b = case[:4]
+        extra = case[4] if len(case) > 4 else {}
         kw = synthetic.REFERENCE_PACKAGE if src == "package" else synthetic.burn_inputs(src)
         st, air = O.air_from_inputs(kw["burn_amount"], kw["mint_amount"], kw["tx_prefix_hash"],
                                     kw["recipient_address"], kw["secret"], kw["network_id"],
                                     kw["target_chain_id"], kw["commitment_version"])
         assert st == 0
-        opts = O.options(blowup=b)
+        opts = O.options(blowup=b, **extra)
         st, proof = O.prove(air, n, opts)
         assert st == 0 and O.verify(air, proof, opts) == 0, name
         rec = {"name": name, "source": src, "n": n, "blowup": b, "len": len(proof),
                "sha256": hashlib.sha256(proof).hexdigest()}
+        if extra:
+            rec["options"] = extra
         if n <= 64:
             rec["proof_hex"] = proof.hex()
         out.append(rec)

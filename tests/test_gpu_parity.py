@@ -125,7 +125,10 @@ def test_prove_trace_bytes_match_oracle(prover, src, n, blowup):
 @pytest.mark.parametrize("case", json.load(open(os.path.join(GOLD, "proofs.json"))), ids=lambda c: c["name"])
 def test_prove_burn_mint_matches_golden(prover, case):
     kw = synthetic.REFERENCE_PACKAGE if case["source"] == "package" else synthetic.burn_inputs(case["source"])
-    with_blowup(prover, case["blowup"])
+    o = with_blowup(prover, case["blowup"])
+    names = {"field_extension": "field_extension", "num_queries": "num_queries"}
+    for k, v in case.get("options", {}).items():
+        setattr(o, names[k], v)
     proof = prover.prove_burn_mint(**kw, trace_length=case["n"]).to_bytes()
     assert len(proof) == case["len"]
     assert hashlib.sha256(proof).hexdigest() == case["sha256"]
@@ -261,6 +264,45 @@ def test_generate_from_data_package_matches_golden(prover, tmp_path):
     assert res[1][0] is None and not res[1][1].is_valid
     assert res[2][0] is None and isinstance(res[2][1], K.PackageError)
     assert bytes(res[0][0]["proof_data"]) == bytes(res[3][0]["proof_data"]) == data
+
+
+@pytest.mark.parametrize("n,kw", [(64, dict(blowup_factor=8)), (256, dict(blowup_factor=4)),
+                                  (1024, dict(blowup_factor=16, num_queries=24)),
+                                  (2048, dict(blowup_factor=8, fri_remainder_max_degree=255)),
+                                  (128, dict(blowup_factor=2, grinding_factor=0))])
+def test_quadratic_extension_matches_oracle(prover, n, kw):
+    """FieldExtension::Quadratic: GPU bytes == oracle bytes (batch of 3 statements), and both the
+    product verifier and the oracle verifier accept"""
+    import xfgstark
+    o = xfgstark.ProofOptions.reference()
+    o.field_extension = 2
+    for k, v in kw.items():
+        setattr(o, k, v)
+    prover._options = o
+    kws = [synthetic.burn_inputs(1300 + n + i) for i in range(3)]
+    res = prover.prove_batch(kws, trace_length=n)
+    oo = O.options(num_queries=o.num_queries, blowup=o.blowup_factor, grinding=o.grinding_factor, field_extension=2,
+                   fri_rem_max_deg=o.fri_remainder_max_degree)
+    v = xfgstark.XfgBurnMintVerifier(proof_options=o)
+    for kw_, pr in zip(kws, res):
+        st, want = O.prove(oracle_air(kw_), n, oo)
+        assert st == 0 and pr.to_bytes() == want
+        assert v.verify_burn_mint(pr, **kw_)
+
+
+def test_config5_quadratic_2p20_blowup16(prover):
+    """BASELINE config 5 shape: n = 2^20, blowup 16, quadratic extension, 24 queries (~100-bit
+    conjectured security): the proof verifies (product + oracle verifiers) and is deterministic"""
+    import xfgstark
+    o = xfgstark.ProofOptions.reference()
+    o.field_extension, o.blowup_factor, o.num_queries = 2, 16, 24
+    prover._options = o
+    kw = synthetic.burn_inputs(5005)
+    p1 = prover.prove_burn_mint(**kw, trace_length=1 << 20).to_bytes()
+    assert xfgstark.XfgBurnMintVerifier(proof_options=o).verify_burn_mint(p1, **kw)
+    oo = O.options(num_queries=24, blowup=16, field_extension=2)
+    assert O.verify(oracle_air(kw), p1, oo) == 0
+    assert prover.prove_burn_mint(**kw, trace_length=1 << 20).to_bytes() == p1
 
 
 def test_rejects_options_the_reference_rejects(prover):

@@ -116,7 +116,7 @@ def test_oracle_proof_fixtures(case):
     kw = synthetic.REFERENCE_PACKAGE if case["source"] == "package" else synthetic.burn_inputs(case["source"])
     st, air = O.air_from_inputs(kw["burn_amount"], kw["mint_amount"], kw["tx_prefix_hash"],
                                 kw["recipient_address"], kw["secret"])
-    opts = O.options(blowup=case["blowup"])
+    opts = O.options(blowup=case["blowup"], **case.get("options", {}))
     st, proof = O.prove(air, case["n"], opts)
     assert st == 0
     assert hashlib.sha256(proof).hexdigest() == case["sha256"] and len(proof) == case["len"]

@@ -40,7 +40,7 @@ def _oracle_proof(kw, n, **opts):
 def _opts(X, **kw):
     o = X.ProofOptions.reference()
     names = {"blowup": "blowup_factor", "fri_rem_max_deg": "fri_remainder_max_degree", "grinding": "grinding_factor",
-             "num_queries": "num_queries"}
+             "num_queries": "num_queries", "field_extension": "field_extension"}
     for k, v in kw.items():
         setattr(o, names[k], v)
     return o
@@ -126,7 +126,9 @@ def test_verifier_accepts_golden_fixture(X):
 
 
 @pytest.mark.parametrize("n,kw", [(64, dict(blowup=4)), (1024, dict()), (2048, dict(fri_rem_max_deg=255)),
-                                  (256, dict(blowup=16, num_queries=24)), (512, dict(blowup=2, grinding=0))])
+                                  (256, dict(blowup=16, num_queries=24)), (512, dict(blowup=2, grinding=0)),
+                                  (64, dict(field_extension=2)), (1024, dict(field_extension=2, blowup=16, num_queries=24)),
+                                  (2048, dict(field_extension=2, fri_rem_max_deg=127))])
 def test_verifier_accepts_oracle_proofs(X, n, kw):
     kws = synthetic.burn_inputs(n + len(kw))
     proof = _oracle_proof(kws, n, **kw)
@@ -169,6 +171,27 @@ def test_verifier_rejects_tampering_with_reference_errors(X):
     # options outside the acceptable set
     ok, err, _ = X.XfgBurnMintVerifier(proof_options=_opts(X, num_queries=41)).verify_with_details(proof, air)
     assert not ok and err == "UnacceptableProofOptions"
+
+
+def test_verifier_quadratic_tampering(X):
+    """FieldExtension::Quadratic proofs (E-valued OOD frame, composition rows, FRI layers)"""
+    kws = synthetic.burn_inputs(77)
+    kw = dict(field_extension=2)
+    proof = _oracle_proof(kws, 256, **kw)
+    air = _statement(X, kws)
+    v = X.XfgBurnMintVerifier(proof_options=_opts(X, **kw))
+    assert v.verify_with_public_inputs(proof, air)
+    sec = _sections(proof)
+    for name, want in {"constraint_rows": "ConstraintQueryDoesNotMatchCommitment",
+                       "ood": "InconsistentOodConstraintEvaluations", "hz": "InconsistentOodConstraintEvaluations",
+                       "fri_vals0": "FriVerificationFailed", "remainder": "FriVerificationFailed"}.items():
+        for at in (sec[name][0] + 1, sec[name][0] + 9):  # first and second coordinate of an element
+            ok, err, _ = v.verify_with_details(_flip(proof, at), air)
+            assert not ok and err.startswith(want), (name, at, err)
+    # the same proof is not acceptable as a base-field proof and vice versa
+    assert not X.XfgBurnMintVerifier().verify_with_public_inputs(proof, air)
+    p = X.StarkProof.from_bytes(proof)
+    assert p.options.field_extension == 2 and p.trace_length == 256
 
 
 def test_batch_verify_mixed(X):

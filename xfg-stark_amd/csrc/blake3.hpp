@@ -95,18 +95,35 @@ __host__ __device__ __forceinline__ Digest b3_merge(const Digest& a, const Diges
     for (int i = 0; i < 8; i++) { m[i] = a.w[i]; m[8 + i] = b.w[i]; }
     return b3_hash_block(m, 64);
 }
-// Blake3_256::hash_elements for up to 8 field elements (one block)
+// Blake3_256::hash_elements for up to 16 field elements (one or two blocks of one chunk)
 template <int K>
 __host__ __device__ __forceinline__ Digest b3_hash_elems(const uint64_t* e) {
-    static_assert(K >= 1 && K <= 8, "single-block element hash");
+    static_assert(K >= 1 && K <= 16, "one- or two-block element hash");
     uint32_t m[16];
+    constexpr int K0 = K <= 8 ? K : 8;
 #pragma unroll
     for (int i = 0; i < 8; i++) {
-        uint64_t v = i < K ? e[i] : 0;
+        uint64_t v = i < K0 ? e[i] : 0;
         m[2 * i] = (uint32_t)v;
         m[2 * i + 1] = (uint32_t)(v >> 32);
     }
-    return b3_hash_block(m, 8 * K);
+    if constexpr (K <= 8) {
+        return b3_hash_block(m, 8 * K);
+    } else {
+        const uint32_t iv[8] = {XFG_B3_IV0, XFG_B3_IV1, XFG_B3_IV2, XFG_B3_IV3,
+                                XFG_B3_IV4, XFG_B3_IV5, XFG_B3_IV6, XFG_B3_IV7};
+        uint32_t cv[8];
+        b3_compress(iv, m, 64, 0, B3_CHUNK_START, cv);
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            uint64_t v = 8 + i < K ? e[8 + i] : 0;
+            m[2 * i] = (uint32_t)v;
+            m[2 * i + 1] = (uint32_t)(v >> 32);
+        }
+        Digest d;
+        b3_compress(cv, m, 8 * (K - 8), 0, B3_CHUNK_END | B3_ROOT, d.w);
+        return d;
+    }
 }
 
 }  // namespace xfg

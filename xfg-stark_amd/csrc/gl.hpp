@@ -75,4 +75,65 @@ __host__ __device__ inline u64 gl_inv(u64 a) { return gl_pow(a, P - 2); }
 // winter-math get_root_of_unity(k): primitive 2^k-th root
 __host__ __device__ inline u64 gl_root(unsigned k) { return gl_pow(TWO_ADIC_ROOT, 1ULL << (32 - k)); }
 
+// ---- quadratic extension E = F[phi] / (phi^2 - phi + 2) (winter-math f64 QuadExtension):
+// (a0 + a1 phi)(b0 + b1 phi) = (a0 b0 - 2 a1 b1) + ((a0 + a1)(b0 + b1) - a0 b0) phi
+struct E2 {
+    u64 a, b;
+};
+__host__ __device__ __forceinline__ E2 e2(u64 a, u64 b = 0) { return E2{a, b}; }
+__host__ __device__ __forceinline__ E2 e2_add(E2 x, E2 y) { return E2{gl_add(x.a, y.a), gl_add(x.b, y.b)}; }
+__host__ __device__ __forceinline__ E2 e2_sub(E2 x, E2 y) { return E2{gl_sub(x.a, y.a), gl_sub(x.b, y.b)}; }
+__host__ __device__ __forceinline__ E2 e2_mulb(E2 x, u64 s) { return E2{gl_mul(x.a, s), gl_mul(x.b, s)}; }
+__host__ __device__ __forceinline__ E2 e2_mul(E2 x, E2 y) {
+    const u64 a0b0 = gl_mul(x.a, y.a), a1b1 = gl_mul(x.b, y.b);
+    const u64 m = gl_mul(gl_add(x.a, x.b), gl_add(y.a, y.b));
+    return E2{gl_sub(a0b0, gl_add(a1b1, a1b1)), gl_sub(m, a0b0)};
+}
+__host__ __device__ inline E2 e2_inv(E2 x) {
+    // frob(x) = (a0 + a1) - a1 phi; x * frob(x) is in F
+    const E2 f{gl_add(x.a, x.b), gl_neg(x.b)};
+    return e2_mulb(f, gl_inv(e2_mul(x, f).a));
+}
+__host__ __device__ inline E2 e2_pow(E2 b, u64 e) {
+    E2 r{1, 0};
+    while (e) {
+        if (e & 1) r = e2_mul(r, b);
+        b = e2_mul(b, b);
+        e >>= 1;
+    }
+    return r;
+}
+__host__ __device__ __forceinline__ bool e2_eq(E2 x, E2 y) { return x.a == y.a && x.b == y.b; }
+
+// field element of extension degree D (1 = base, 2 = quadratic) for D-templated kernels
+template <int D>
+struct FE;
+template <>
+struct FE<1> {
+    u64 a;
+    __host__ __device__ __forceinline__ static FE zero() { return FE{0}; }
+    __host__ __device__ __forceinline__ static FE load(const u64* p) { return FE{p[0]}; }
+    __host__ __device__ __forceinline__ void store(u64* p) const { p[0] = a; }
+    __host__ __device__ __forceinline__ u64 c(int) const { return a; }
+};
+template <>
+struct FE<2> {
+    u64 a, b;
+    __host__ __device__ __forceinline__ static FE zero() { return FE{0, 0}; }
+    __host__ __device__ __forceinline__ static FE load(const u64* p) { return FE{p[0], p[1]}; }
+    __host__ __device__ __forceinline__ void store(u64* p) const { p[0] = a; p[1] = b; }
+    __host__ __device__ __forceinline__ u64 c(int i) const { return i ? b : a; }
+};
+__host__ __device__ __forceinline__ FE<1> fe_add(FE<1> x, FE<1> y) { return FE<1>{gl_add(x.a, y.a)}; }
+__host__ __device__ __forceinline__ FE<1> fe_sub(FE<1> x, FE<1> y) { return FE<1>{gl_sub(x.a, y.a)}; }
+__host__ __device__ __forceinline__ FE<1> fe_mul(FE<1> x, FE<1> y) { return FE<1>{gl_mul(x.a, y.a)}; }
+__host__ __device__ __forceinline__ FE<1> fe_mulb(FE<1> x, u64 s) { return FE<1>{gl_mul(x.a, s)}; }
+__host__ __device__ __forceinline__ FE<2> fe_add(FE<2> x, FE<2> y) { return FE<2>{gl_add(x.a, y.a), gl_add(x.b, y.b)}; }
+__host__ __device__ __forceinline__ FE<2> fe_sub(FE<2> x, FE<2> y) { return FE<2>{gl_sub(x.a, y.a), gl_sub(x.b, y.b)}; }
+__host__ __device__ __forceinline__ FE<2> fe_mulb(FE<2> x, u64 s) { return FE<2>{gl_mul(x.a, s), gl_mul(x.b, s)}; }
+__host__ __device__ __forceinline__ FE<2> fe_mul(FE<2> x, FE<2> y) {
+    E2 r = e2_mul(E2{x.a, x.b}, E2{y.a, y.b});
+    return FE<2>{r.a, r.b};
+}
+
 }  // namespace xfg

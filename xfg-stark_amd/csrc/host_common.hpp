@@ -35,7 +35,7 @@ static inline const char* check_options(u64 n, const Opts& o) {
     if (!is_pow2(o.beta) || o.beta < 2 || o.beta > 16) return "blowup factor must be a power of two in [2, 16]";
     if (o.q < 1 || o.q > 255) return "number of queries must be in [1, 255]";
     if (o.grind > 32) return "grinding factor cannot be greater than 32";
-    if (o.ext != 1) return "only FieldExtension::None is supported by this prover";
+    if (o.ext != 1 && o.ext != 2) return "field extension must be None (1) or Quadratic (2)";
     if (o.fold != 8) return "only FRI folding factor 8 is supported by this prover";
     if (o.remdeg > 255 || !is_pow2(o.remdeg + 1)) return "FRI remainder max degree must be one less than a power of two";
     if (o.q >= n * o.beta) return "number of queries must be smaller than the LDE domain size";
@@ -85,6 +85,21 @@ struct Coin {
             u64 x = (u64)v.w[0] | ((u64)v.w[1] << 32);
             if (x < P) {
                 out = x;
+                return true;
+            }
+        }
+        return false;
+    }
+    // draw::<E>() for extension degree d: the first 8 d digest bytes as d LE elements, retried
+    // while any of them is >= p (QuadExtension::from_random_bytes); out[d]
+    bool draw_e(u64* out, int d) {
+        if (d == 1) return draw(out[0]);
+        for (int i = 0; i < 1000; i++) {
+            Digest v = next();
+            const u64 x = (u64)v.w[0] | ((u64)v.w[1] << 32), y = (u64)v.w[2] | ((u64)v.w[3] << 32);
+            if (x < P && y < P) {
+                out[0] = x;
+                out[1] = y;
                 return true;
             }
         }

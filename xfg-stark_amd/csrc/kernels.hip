@@ -154,6 +154,7 @@ u64 launch_leaves_lde(const u64* lde, int nc, Digest* nodes, u64 node_stride, in
     const int wmin = up_wmin(T);
     dim3 g((unsigned)(n / 2 / T), npoly), b((unsigned)T);
     if (nc == 7) { XFG_LOGB_DISPATCH(leaves_lde_kernel, 7, logbeta, g, b, 0, s, lde, nodes, node_stride, logn, wmin) }
+    else if (nc == 2) { XFG_LOGB_DISPATCH(leaves_lde_kernel, 2, logbeta, g, b, 0, s, lde, nodes, node_stride, logn, wmin) }
     else { XFG_LOGB_DISPATCH(leaves_lde_kernel, 1, logbeta, g, b, 0, s, lde, nodes, node_stride, logn, wmin) }
     XFG_CHECK_LAUNCH();
     return n / 2 / T * wmin;
@@ -163,6 +164,7 @@ void launch_open_rows(const u64* lde, int nc, const u64* entries, u64 count, Dig
     if (!count) return;
     dim3 g((unsigned)((count + 63) / 64)), b(64);
     if (nc == 7) { XFG_LOGB_DISPATCH(open_rows_kernel, 7, logbeta, g, b, 0, s, lde, entries, count, out, logn) }
+    else if (nc == 2) { XFG_LOGB_DISPATCH(open_rows_kernel, 2, logbeta, g, b, 0, s, lde, entries, count, out, logn) }
     else { XFG_LOGB_DISPATCH(open_rows_kernel, 1, logbeta, g, b, 0, s, lde, entries, count, out, logn) }
     XFG_CHECK_LAUNCH();
 }
@@ -243,28 +245,37 @@ __device__ __forceinline__ u64 layer_at(const u64* base, bool coset_major, int l
 
 // FRI layer leaves (hash_values::<H, E, 8> over transpose_slice rows): leaf i = H(values at
 // natural indices i + k*rows, k < 8). All leaves are stored (layers are N/8 and smaller).
-__global__ __launch_bounds__(256) void fri_leaves_kernel(const u64* vals, u64 val_stride, int coset_major, int logn,
-                                                         int logbeta, u64 rows, Digest* nodes_all, u64 node_stride,
-                                                         int wmin) {
+// E-valued layers are D coordinate planes `comp_stride` elements apart (per proof: D planes)
+template <int D>
+__global__ __launch_bounds__(256) void fri_leaves_kernel(const u64* vals, u64 val_stride, u64 comp_stride,
+                                                         int coset_major, int logn, int logbeta, u64 rows,
+                                                         Digest* nodes_all, u64 node_stride, int wmin) {
     __shared__ Digest lds[256];
     const int proof = blockIdx.y;
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;  // grid covers rows exactly
     const u64* base = vals + (u64)proof * val_stride;
-    u64 v[8];
+    u64 v[8 * D];
 #pragma unroll
-    for (int k = 0; k < 8; k++) v[k] = layer_at(base, coset_major, logn, logbeta, i + (u64)k * rows);
-    Digest d = b3_hash_elems<8>(v);
+    for (int k = 0; k < 8; k++)
+#pragma unroll
+        for (int c = 0; c < D; c++)
+            v[k * D + c] = layer_at(base + c * comp_stride, coset_major, logn, logbeta, i + (u64)k * rows);
+    Digest d = b3_hash_elems<8 * D>(v);
     Digest* nodes = nodes_all + (u64)proof * node_stride;
     nodes[rows + i] = d;
     block_tree_up(d, nodes, rows, lds, wmin);
 }
-u64 launch_fri_leaves(const u64* vals, u64 val_stride, bool coset_major, int logn, int logbeta, u64 rows,
-                      Digest* nodes, u64 node_stride, int npoly, hipStream_t s) {
+u64 launch_fri_leaves(const u64* vals, u64 val_stride, u64 comp_stride, bool coset_major, int logn, int logbeta,
+                      u64 rows, Digest* nodes, u64 node_stride, int npoly, int ext, hipStream_t s) {
     const u64 T = std::min<u64>(256, rows);
     const int wmin = up_wmin(T);
     dim3 g((unsigned)(rows / T), npoly);
-    hipLaunchKernelGGL(fri_leaves_kernel, g, dim3((unsigned)T), 0, s, vals, val_stride, coset_major ? 1 : 0, logn,
-                       logbeta, rows, nodes, node_stride, wmin);
+    if (ext == 2)
+        hipLaunchKernelGGL(fri_leaves_kernel<2>, g, dim3((unsigned)T), 0, s, vals, val_stride, comp_stride,
+                           coset_major ? 1 : 0, logn, logbeta, rows, nodes, node_stride, wmin);
+    else
+        hipLaunchKernelGGL(fri_leaves_kernel<1>, g, dim3((unsigned)T), 0, s, vals, val_stride, comp_stride,
+                           coset_major ? 1 : 0, logn, logbeta, rows, nodes, node_stride, wmin);
     XFG_CHECK_LAUNCH();
     return rows / T * wmin;
 }
@@ -305,13 +316,17 @@ struct CeArgs {
 // (ce_to_lde_blowup = beta/2: CE point i is LDE row i*beta/2, i.e. coset t = par*beta/2, row m).
 // Threads walk m fastest inside one parity so the coset-major LDE reads are coalesced.
 // The divisor inverses are data independent and come from a per-(n, beta) table.
+// D = extension degree of the composition coefficients (1: FieldExtension::None, 2: Quadratic);
+// the evaluations are written as D coordinate planes ce[proof][c][nce].
+template <int D>
 __global__ __launch_bounds__(256) void constraint_eval_kernel(CeArgs a) {
+    using F = FE<D>;
     const u64 n = 1ULL << a.logn, nce = 2 * n;
     const int proof = blockIdx.y;
     const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;  // grid covers nce exactly
     const u64 par = g >> a.logn, m = g & (n - 1), i = 2 * m + par;
     const AirConst& A = a.air[proof];
-    const u64* co = a.coeffs + (u64)proof * 15;
+    const u64* co = a.coeffs + (u64)proof * 15 * D;
     const u64 beta = 1ULL << a.logbeta;
     const u64* lde = a.lde + (u64)proof * 7 * beta * n;
     const u64 t = par * (beta / 2), mn = (m + 1) & (n - 1);
@@ -321,41 +336,40 @@ __global__ __launch_bounds__(256) void constraint_eval_kernel(CeArgs a) {
     const u64 nxt4 = lde[((4ULL << a.logbeta) + t) * n + mn];
     // XfgBurnMintAir::evaluate_transition (reference src/burn_mint_air.rs:335-378)
     const u64 std_burn = 8000000ULL, large_burn = 8000000000ULL;
-    u64 r0 = gl_mul(gl_sub(cur[0], std_burn), gl_sub(cur[0], large_burn));
-    u64 r1 = gl_sub(cur[1], cur[0]);
-    u64 r2 = gl_sub(cur[2], A.pub[2] & 0xFFFFFFFFULL);
-    u64 r3 = gl_sub(cur[3], A.pub[3] & 0xFFFFFFFFULL);
-    u64 d = gl_sub(nxt4, cur[4]);
-    u64 r4 = gl_mul(d, gl_sub(d, 1));
-    u64 r5 = gl_sub(cur[5], A.nullifier);
-    u64 r6 = gl_sub(cur[6], A.commitment);
-    u64 tr = gl_mul(co[0], r0);
-    tr = gl_add(tr, gl_mul(co[1], r1));
-    tr = gl_add(tr, gl_mul(co[2], r2));
-    tr = gl_add(tr, gl_mul(co[3], r3));
-    tr = gl_add(tr, gl_mul(co[4], r4));
-    tr = gl_add(tr, gl_mul(co[5], r5));
-    tr = gl_add(tr, gl_mul(co[6], r6));
+    u64 r[7];
+    r[0] = gl_mul(gl_sub(cur[0], std_burn), gl_sub(cur[0], large_burn));
+    r[1] = gl_sub(cur[1], cur[0]);
+    r[2] = gl_sub(cur[2], A.pub[2] & 0xFFFFFFFFULL);
+    r[3] = gl_sub(cur[3], A.pub[3] & 0xFFFFFFFFULL);
+    const u64 d = gl_sub(nxt4, cur[4]);
+    r[4] = gl_mul(d, gl_sub(d, 1));
+    r[5] = gl_sub(cur[5], A.nullifier);
+    r[6] = gl_sub(cur[6], A.commitment);
+    F tr = F::zero();
+#pragma unroll
+    for (int c = 0; c < 7; c++) tr = fe_add(tr, fe_mulb(F::load(co + c * D), r[c]));
     // assertions (src/burn_mint_air.rs:380-395): step 0 on columns 0..6, step n-1 on column 4
     const u64 v0[7] = {A.pub[0], A.pub[1], A.pub[2], A.pub[3], 0, A.nullifier, A.commitment};
-    u64 b0 = 0;
+    F b0 = F::zero();
 #pragma unroll
-    for (int c = 0; c < 7; c++) b0 = gl_add(b0, gl_mul(co[7 + c], gl_sub(cur[c], v0[c])));
-    u64 b1 = gl_mul(co[14], gl_sub(cur[4], 3));
+    for (int c = 0; c < 7; c++) b0 = fe_add(b0, fe_mulb(F::load(co + (7 + c) * D), gl_sub(cur[c], v0[c])));
+    const F b1 = fe_mulb(F::load(co + 14 * D), gl_sub(cur[4], 3));
     const u64 di = par * n + m;
-    u64 val = gl_mul(tr, a.div[di]);
-    val = gl_add(val, gl_mul(b0, a.div[nce + di]));
-    val = gl_add(val, gl_mul(b1, a.div[2 * nce + di]));
-    a.ce[(u64)proof * nce + i] = val;
+    F val = fe_mulb(tr, a.div[di]);
+    val = fe_add(val, fe_mulb(b0, a.div[nce + di]));
+    val = fe_add(val, fe_mulb(b1, a.div[2 * nce + di]));
+#pragma unroll
+    for (int c = 0; c < D; c++) a.ce[((u64)proof * D + c) * nce + i] = val.c(c);
 }
 void launch_constraint_eval(const u64* lde, const AirConst* air, const u64* coeffs, const u64* div, u64* ce, int logn,
-                            int logbeta, int npoly, hipStream_t s) {
+                            int logbeta, int npoly, int ext, hipStream_t s) {
     CeArgs a;
     a.lde = lde; a.air = air; a.coeffs = coeffs; a.div = div; a.ce = ce; a.logn = logn; a.logbeta = logbeta;
     u64 nce = 2ULL << logn;
     int threads = nce < 256 ? (int)nce : 256;
     dim3 g((unsigned)(nce / threads), npoly);
-    hipLaunchKernelGGL(constraint_eval_kernel, g, dim3(threads), 0, s, a);
+    if (ext == 2) hipLaunchKernelGGL(constraint_eval_kernel<2>, g, dim3(threads), 0, s, a);
+    else hipLaunchKernelGGL(constraint_eval_kernel<1>, g, dim3(threads), 0, s, a);
     XFG_CHECK_LAUNCH();
 }
 
@@ -373,71 +387,101 @@ __device__ __forceinline__ u64 shfl_xor_u64(u64 v, int m, int w) {
     return (u64)lo | ((u64)hi << 32);
 }
 
+template <int D>
+__device__ __forceinline__ FE<D> fe_pow(FE<D> b, u64 e) {
+    FE<D> r = FE<D>::zero();
+    r.a = 1;
+    while (e) {
+        if (e & 1) r = fe_mul(r, b);
+        b = fe_mul(b, b);
+        e >>= 1;
+    }
+    return r;
+}
+template <int D>
+__device__ __forceinline__ FE<D> fe_plane(const u64* planes, u64 plane_stride, u64 j) {  // coordinates from planes
+    FE<D> v;
+    v.a = planes[j];
+    if constexpr (D == 2) v.b = planes[plane_stride + j];
+    return v;
+}
+
+// zpts [proof][2][D] = (z, z g); coef [proof][7][n] (base); hcoef [proof][D][n];
+// partial [proof][block][15][D]
+template <int D>
 __global__ __launch_bounds__(256) void ood_kernel(const u64* coef, const u64* hcoef, const u64* zpts, u64* partial,
                                                   int logn) {
-    __shared__ u64 zb[4];
-    __shared__ u64 red[4][15];
+    using F = FE<D>;
+    __shared__ u64 zb[4][D];
+    __shared__ u64 red[4][15][D];
     const u64 n = 1ULL << logn;
     const int proof = blockIdx.y, t = threadIdx.x, T = blockDim.x;
     const u64 base = (u64)blockIdx.x * T * OOD_R;
-    const u64 z = zpts[2 * proof], zg = zpts[2 * proof + 1];
+    const F z = F::load(zpts + (u64)proof * 2 * D), zg = F::load(zpts + (u64)proof * 2 * D + D);
     if (t == 0) {
-        zb[0] = gl_pow(z, base);
-        zb[1] = gl_pow(zg, base);
-        zb[2] = gl_pow(z, (u64)T);
-        zb[3] = gl_pow(zg, (u64)T);
+        fe_pow(z, base).store(zb[0]);
+        fe_pow(zg, base).store(zb[1]);
+        fe_pow(z, (u64)T).store(zb[2]);
+        fe_pow(zg, (u64)T).store(zb[3]);
     }
     __syncthreads();
-    u64 pz = gl_mul(zb[0], gl_pow(z, (u64)t)), pzg = gl_mul(zb[1], gl_pow(zg, (u64)t));
-    const u64 zT = zb[2], zgT = zb[3];
+    F pz = fe_mul(F::load(zb[0]), fe_pow(z, (u64)t)), pzg = fe_mul(F::load(zb[1]), fe_pow(zg, (u64)t));
+    const F zT = F::load(zb[2]), zgT = F::load(zb[3]);
     const u64* co = coef + (u64)proof * 7 * n;
-    const u64* h = hcoef + (u64)proof * n;
-    u64 acc[15];
+    const u64* h = hcoef + (u64)proof * D * n;
+    F acc[15];
 #pragma unroll
-    for (int q = 0; q < 15; q++) acc[q] = 0;
+    for (int q = 0; q < 15; q++) acc[q] = F::zero();
 #pragma unroll 2
     for (int r = 0; r < OOD_R; r++) {
         const u64 j = base + (u64)r * T + t;
 #pragma unroll
         for (int c = 0; c < 7; c++) {
             u64 v = co[(u64)c * n + j];
-            acc[2 * c] = gl_add(acc[2 * c], gl_mul(v, pz));
-            acc[2 * c + 1] = gl_add(acc[2 * c + 1], gl_mul(v, pzg));
+            acc[2 * c] = fe_add(acc[2 * c], fe_mulb(pz, v));
+            acc[2 * c + 1] = fe_add(acc[2 * c + 1], fe_mulb(pzg, v));
         }
-        acc[14] = gl_add(acc[14], gl_mul(h[j], pz));
-        pz = gl_mul(pz, zT);
-        pzg = gl_mul(pzg, zgT);
+        acc[14] = fe_add(acc[14], fe_mul(fe_plane<D>(h, n, j), pz));
+        pz = fe_mul(pz, zT);
+        pzg = fe_mul(pzg, zgT);
     }
     // wave reduction, then across the (up to 4) waves
     const int W = T < 64 ? T : 64;
     for (int m = W / 2; m > 0; m >>= 1) {
 #pragma unroll
-        for (int q = 0; q < 15; q++) acc[q] = gl_add(acc[q], shfl_xor_u64(acc[q], m, W));
+        for (int q = 0; q < 15; q++) {
+            acc[q].a = gl_add(acc[q].a, shfl_xor_u64(acc[q].a, m, W));
+            if constexpr (D == 2) acc[q].b = gl_add(acc[q].b, shfl_xor_u64(acc[q].b, m, W));
+        }
     }
     if ((t & 63) == 0) {
 #pragma unroll
-        for (int q = 0; q < 15; q++) red[t >> 6][q] = acc[q];
+        for (int q = 0; q < 15; q++) acc[q].store(red[t >> 6][q]);
     }
     __syncthreads();
-    for (int q = t; q < 15; q += T) {  // T may be below 15 for short traces
-        u64 v = red[0][q];
-        for (int w = 1; w < (T + 63) / 64; w++) v = gl_add(v, red[w][q]);
-        partial[((u64)proof * gridDim.x + blockIdx.x) * 15 + q] = v;
+    for (int qc = t; qc < 15 * D; qc += T) {  // T may be below 15 D for short traces
+        const int q = qc / D, cc = qc % D;
+        u64 v = red[0][q][cc];
+        for (int w = 1; w < (T + 63) / 64; w++) v = gl_add(v, red[w][q][cc]);
+        partial[((u64)proof * gridDim.x + blockIdx.x) * 15 * D + qc] = v;
     }
 }
-__global__ void ood_final_kernel(const u64* partial, int nblk, u64* ood) {
+__global__ void ood_final_kernel(const u64* partial, int nblk, int d, u64* ood) {
     const int proof = blockIdx.x, q = threadIdx.x;
-    if (q >= 15) return;
+    if (q >= 15 * d) return;
     u64 s = 0;
-    for (int b = 0; b < nblk; b++) s = gl_add(s, partial[((u64)proof * nblk + b) * 15 + q]);
-    ood[(u64)proof * 15 + q] = s;
+    for (int b = 0; b < nblk; b++) s = gl_add(s, partial[((u64)proof * nblk + b) * 15 * d + q]);
+    ood[(u64)proof * 15 * d + q] = s;
 }
 void launch_ood(const u64* coef, const u64* hcoef, const u64* zpts, u64* partial, u64* ood, int logn, int npoly,
-                hipStream_t s) {
+                int ext, hipStream_t s) {
     const u64 n = 1ULL << logn;
     const int T = ood_threads(n), nblk = (int)(n / ((u64)T * OOD_R));
-    hipLaunchKernelGGL(ood_kernel, dim3(nblk, npoly), dim3(T), 0, s, coef, hcoef, zpts, partial, logn);
-    hipLaunchKernelGGL(ood_final_kernel, dim3(npoly), dim3(64), 0, s, partial, nblk, ood);
+    if (ext == 2)
+        hipLaunchKernelGGL(ood_kernel<2>, dim3(nblk, npoly), dim3(T), 0, s, coef, hcoef, zpts, partial, logn);
+    else
+        hipLaunchKernelGGL(ood_kernel<1>, dim3(nblk, npoly), dim3(T), 0, s, coef, hcoef, zpts, partial, logn);
+    hipLaunchKernelGGL(ood_final_kernel, dim3(npoly), dim3(64), 0, s, partial, nblk, ext, ood);
     XFG_CHECK_LAUNCH();
 }
 u64 ood_partial_count(int logn) {
@@ -454,140 +498,168 @@ u64 ood_partial_count(int logn) {
 // (deep_carry_kernel). Inside a block every thread owns OOD_R consecutive indices: a backward
 // Horner pass gives its chunk map Q_out = L + z^R Q_in, a suffix scan over threads with the
 // uniform multiplier z^R gives each thread's Q_in, and a second backward pass writes d_k.
-// one block per proof, one thread per OOD block b: block sums, suffix sum over blocks, weights
+// All of it in E (extension degree D): coefficients, z and the output planes deep[proof][c][n].
+template <int D>
 __global__ __launch_bounds__(1024) void deep_carry_kernel(const u64* partial, const DeepParams* dp, u64* carry,
                                                           int nblk, int logch) {
-    __shared__ u64 S1[1024], S2[1024];
+    using F = FE<D>;
+    __shared__ u64 S1[1024][D], S2[1024][D];
     const int proof = blockIdx.x, b = threadIdx.x;
-    const DeepParams P = dp[proof];
-    u64 b1 = 0, b2 = 0;
+    const DeepParams& P = dp[proof];
+    F b1 = F::zero(), b2 = F::zero();
     if (b < nblk) {
-        const u64* pp = partial + ((u64)proof * nblk + b) * 15;
-        u64 t1 = 0, t2 = 0;
+        const u64* pp = partial + ((u64)proof * nblk + b) * 15 * D;
+        F t1 = F::zero(), t2 = F::zero();
 #pragma unroll
         for (int c = 0; c < 7; c++) {
-            t1 = gl_add(t1, gl_mul(P.a[c], pp[2 * c]));
-            t2 = gl_add(t2, gl_mul(P.a[c], pp[2 * c + 1]));
+            const F a = F::load(P.a[c]);
+            t1 = fe_add(t1, fe_mul(a, F::load(pp + 2 * c * D)));
+            t2 = fe_add(t2, fe_mul(a, F::load(pp + (2 * c + 1) * D)));
         }
-        b1 = gl_add(t1, gl_mul(P.gamma, pp[14]));
+        b1 = fe_add(t1, fe_mul(F::load(P.gamma), F::load(pp + 14 * D)));
         b2 = t2;
         if (b == 0) {
-            b1 = gl_sub(b1, P.c1);
-            b2 = gl_sub(b2, P.c2);
+            b1 = fe_sub(b1, F::load(P.c1));
+            b2 = fe_sub(b2, F::load(P.c2));
         }
     }
-    S1[b] = b1;
-    S2[b] = b2;
+    b1.store(S1[b]);
+    b2.store(S2[b]);
     __syncthreads();
     for (int off = 1; off < (int)blockDim.x; off <<= 1) {  // inclusive suffix sums
-        u64 v1 = S1[b], v2 = S2[b];
+        F v1 = F::load(S1[b]), v2 = F::load(S2[b]);
         if (b + off < (int)blockDim.x) {
-            v1 = gl_add(v1, S1[b + off]);
-            v2 = gl_add(v2, S2[b + off]);
+            v1 = fe_add(v1, F::load(S1[b + off]));
+            v2 = fe_add(v2, F::load(S2[b + off]));
         }
         __syncthreads();
-        S1[b] = v1;
-        S2[b] = v2;
+        v1.store(S1[b]);
+        v2.store(S2[b]);
         __syncthreads();
     }
     if (b < nblk) {
         const u64 e = (u64)(b + 1) << logch;  // carry into block b: z^-e * sum over blocks after b
-        const u64 x1 = b + 1 < nblk ? S1[b + 1] : 0, x2 = b + 1 < nblk ? S2[b + 1] : 0;
-        carry[((u64)proof * nblk + b) * 2] = gl_mul(x1, gl_pow(P.zinv, e));
-        carry[((u64)proof * nblk + b) * 2 + 1] = gl_mul(x2, gl_pow(P.zginv, e));
+        const F x1 = b + 1 < nblk ? F::load(S1[b + 1]) : F::zero();
+        const F x2 = b + 1 < nblk ? F::load(S2[b + 1]) : F::zero();
+        fe_mul(x1, fe_pow(F::load(P.zinv), e)).store(carry + (((u64)proof * nblk + b) * 2) * D);
+        fe_mul(x2, fe_pow(F::load(P.zginv), e)).store(carry + (((u64)proof * nblk + b) * 2 + 1) * D);
     }
 }
 __device__ __forceinline__ int dpad(int i) { return i + i / OOD_R; }  // chunk stride R+1: no bank pile-up
+template <int D>
 __global__ __launch_bounds__(256) void deep_final_kernel(const u64* coef, const u64* hcoef, const DeepParams* dp,
                                                          const u64* carry, u64* deep, int logn) {
-    constexpr int R = OOD_R, CHMAX = 256 * OOD_R;
-    __shared__ u64 s1[CHMAX + CHMAX / R], s2[CHMAX + CHMAX / R];
-    __shared__ u64 S1[256], S2[256];
+    using F = FE<D>;
+    constexpr int R = OOD_R, CHMAX = 256 * OOD_R, PADN = CHMAX + CHMAX / R;
+    __shared__ u64 s1[D][PADN], s2[D][PADN];
+    __shared__ u64 S1[256][D], S2[256][D];
     const u64 n = 1ULL << logn;
     const int proof = blockIdx.y, t = threadIdx.x, T = blockDim.x;
     const u64 base = (u64)blockIdx.x * T * R;
-    const DeepParams P = dp[proof];
+    const DeepParams& P = dp[proof];
+    const F z = F::load(P.z), zg = F::load(P.zg), gam = F::load(P.gamma);
+    F ac[7];
+#pragma unroll
+    for (int c = 0; c < 7; c++) ac[c] = F::load(P.a[c]);
     const u64* co = coef + (u64)proof * 7 * n;
-    const u64* h = hcoef + (u64)proof * n;
+    const u64* h = hcoef + (u64)proof * D * n;
+    auto lds_ld = [&](u64 (*arr)[PADN], int k) {
+        F v;
+        v.a = arr[0][k];
+        if constexpr (D == 2) v.b = arr[1][k];
+        return v;
+    };
+    auto lds_st = [&](u64 (*arr)[PADN], int k, F v) {
+        arr[0][k] = v.a;
+        if constexpr (D == 2) arr[1][k] = v.b;
+    };
     // 1. P1, P2 (coalesced reads) into LDS
 #pragma unroll 2
     for (int r = 0; r < R; r++) {
         const int li = r * T + t;
         const u64 j = base + li;
-        u64 sacc = 0;
+        F sacc = F::zero();
 #pragma unroll
-        for (int c = 0; c < 7; c++) sacc = gl_add(sacc, gl_mul(P.a[c], co[(u64)c * n + j]));
-        u64 p1 = gl_add(sacc, gl_mul(P.gamma, h[j])), p2 = sacc;
+        for (int c = 0; c < 7; c++) sacc = fe_add(sacc, fe_mulb(ac[c], co[(u64)c * n + j]));
+        F p1 = fe_add(sacc, fe_mul(gam, fe_plane<D>(h, n, j))), p2 = sacc;
         if (j == 0) {
-            p1 = gl_sub(p1, P.c1);
-            p2 = gl_sub(p2, P.c2);
+            p1 = fe_sub(p1, F::load(P.c1));
+            p2 = fe_sub(p2, F::load(P.c2));
         }
-        s1[dpad(li)] = p1;
-        s2[dpad(li)] = p2;
+        lds_st(s1, dpad(li), p1);
+        lds_st(s2, dpad(li), p2);
     }
     __syncthreads();
     // 2. chunk maps: L = sum_i z^i P_{a+i}
     const int a = t * R;
-    u64 L1 = 0, L2 = 0;
+    F L1 = F::zero(), L2 = F::zero();
 #pragma unroll
     for (int i = R - 1; i >= 0; i--) {
-        L1 = gl_add(s1[dpad(a + i)], gl_mul(P.z, L1));
-        L2 = gl_add(s2[dpad(a + i)], gl_mul(P.zg, L2));
+        L1 = fe_add(lds_ld(s1, dpad(a + i)), fe_mul(z, L1));
+        L2 = fe_add(lds_ld(s2, dpad(a + i)), fe_mul(zg, L2));
     }
     // 3. suffix scan over threads, multiplier w = z^R; the block carry enters through the last thread
-    u64 w1 = P.z, w2 = P.zg;
+    F w1 = z, w2 = zg;
 #pragma unroll
     for (int i = 1; i < R; i <<= 1) {
-        w1 = gl_mul(w1, w1);
-        w2 = gl_mul(w2, w2);
+        w1 = fe_mul(w1, w1);
+        w2 = fe_mul(w2, w2);
     }
-    const u64 cin1 = carry[((u64)proof * gridDim.x + blockIdx.x) * 2];
-    const u64 cin2 = carry[((u64)proof * gridDim.x + blockIdx.x) * 2 + 1];
+    const F cin1 = F::load(carry + (((u64)proof * gridDim.x + blockIdx.x) * 2) * D);
+    const F cin2 = F::load(carry + (((u64)proof * gridDim.x + blockIdx.x) * 2 + 1) * D);
     if (t == T - 1) {
-        L1 = gl_add(L1, gl_mul(w1, cin1));
-        L2 = gl_add(L2, gl_mul(w2, cin2));
+        L1 = fe_add(L1, fe_mul(w1, cin1));
+        L2 = fe_add(L2, fe_mul(w2, cin2));
     }
-    S1[t] = L1;
-    S2[t] = L2;
+    L1.store(S1[t]);
+    L2.store(S2[t]);
     __syncthreads();
     for (int off = 1; off < T; off <<= 1) {
-        u64 v1 = S1[t], v2 = S2[t];
+        F v1 = F::load(S1[t]), v2 = F::load(S2[t]);
         if (t + off < T) {
-            v1 = gl_add(v1, gl_mul(w1, S1[t + off]));
-            v2 = gl_add(v2, gl_mul(w2, S2[t + off]));
+            v1 = fe_add(v1, fe_mul(w1, F::load(S1[t + off])));
+            v2 = fe_add(v2, fe_mul(w2, F::load(S2[t + off])));
         }
         __syncthreads();
-        S1[t] = v1;
-        S2[t] = v2;
+        v1.store(S1[t]);
+        v2.store(S2[t]);
         __syncthreads();
-        w1 = gl_mul(w1, w1);
-        w2 = gl_mul(w2, w2);
+        w1 = fe_mul(w1, w1);
+        w2 = fe_mul(w2, w2);
     }
-    u64 q1 = t + 1 < T ? S1[t + 1] : cin1, q2 = t + 1 < T ? S2[t + 1] : cin2;
+    F q1 = t + 1 < T ? F::load(S1[t + 1]) : cin1, q2 = t + 1 < T ? F::load(S2[t + 1]) : cin2;
     // 4. backward pass over the chunk: d_k = q1_k + q2_k, then step to k - 1
 #pragma unroll
     for (int i = R - 1; i >= 0; i--) {
         const int k = dpad(a + i);
-        const u64 p1 = s1[k], p2 = s2[k];
-        s1[k] = gl_add(q1, q2);
-        q1 = gl_add(p1, gl_mul(P.z, q1));
-        q2 = gl_add(p2, gl_mul(P.zg, q2));
+        const F p1 = lds_ld(s1, k), p2 = lds_ld(s2, k);
+        lds_st(s1, k, fe_add(q1, q2));
+        q1 = fe_add(p1, fe_mul(z, q1));
+        q2 = fe_add(p2, fe_mul(zg, q2));
     }
     __syncthreads();
-    u64* out = deep + (u64)proof * n + base;
 #pragma unroll
-    for (int r = 0; r < R; r++) out[r * T + t] = s1[dpad(r * T + t)];
+    for (int c = 0; c < D; c++) {
+        u64* out = deep + ((u64)proof * D + c) * n + base;
+#pragma unroll
+        for (int r = 0; r < R; r++) out[r * T + t] = s1[c][dpad(r * T + t)];
+    }
 }
 void launch_deep(const u64* coef, const u64* hcoef, const DeepParams* dp, const u64* partial, u64* carry, u64* deep,
-                 int logn, int npoly, hipStream_t s) {
+                 int logn, int npoly, int ext, hipStream_t s) {
     const u64 n = 1ULL << logn;
     const int T = ood_threads(n), nblk = (int)(n / ((u64)T * OOD_R));
     int logch = 0;
     while ((1ULL << logch) < (u64)T * OOD_R) logch++;
     int ct = 64;
     while (ct < nblk) ct <<= 1;  // nblk <= 1024 (n <= 2^21, 2048 coefficients per block)
-    hipLaunchKernelGGL(deep_carry_kernel, dim3(npoly), dim3(ct), 0, s, partial, dp, carry, nblk, logch);
-    hipLaunchKernelGGL(deep_final_kernel, dim3(nblk, npoly), dim3(T), 0, s, coef, hcoef, dp, carry, deep, logn);
+    if (ext == 2) {
+        hipLaunchKernelGGL(deep_carry_kernel<2>, dim3(npoly), dim3(ct), 0, s, partial, dp, carry, nblk, logch);
+        hipLaunchKernelGGL(deep_final_kernel<2>, dim3(nblk, npoly), dim3(T), 0, s, coef, hcoef, dp, carry, deep, logn);
+    } else {
+        hipLaunchKernelGGL(deep_carry_kernel<1>, dim3(npoly), dim3(ct), 0, s, partial, dp, carry, nblk, logch);
+        hipLaunchKernelGGL(deep_final_kernel<1>, dim3(nblk, npoly), dim3(T), 0, s, coef, hcoef, dp, carry, deep, logn);
+    }
     XFG_CHECK_LAUNCH();
 }
 
@@ -596,27 +668,34 @@ void launch_deep(const u64* coef, const u64* hcoef, const DeepParams* dp, const 
 // row i = {v_k at 7 w_D^i zeta^k}; c = iDFT_8(v)/8 ; result = sum_j c_j (alpha / (7 w_D^i))^j
 struct FoldArgs {
     const u64* vals;
-    u64 val_stride;
+    u64 val_stride, comp_stride;
     int coset_major, logn, logbeta;
     u64 rows;
     int logD;
-    const u64* alpha7;
-    u64* out;
+    const u64* alpha7;  // [proof][D]: alpha * 7^-1
+    u64* out;           // [proof][D][rows]
     u64 out_stride;
     u64 winv8[4];  // w_8^-k, k < 4
     u64 inv8;
     Tables T;
 };
+template <int D>
 __global__ __launch_bounds__(256) void fri_fold_kernel(FoldArgs a) {
+    using F = FE<D>;
     const int proof = blockIdx.y;
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.rows) return;
     const u64* base = a.vals + (u64)proof * a.val_stride;
-    u64 v[8];
-    // bit-reversed load for an in-register radix-2 DIT inverse DFT of size 8
+    F v[8];
+    // bit-reversed load for an in-register radix-2 DIT inverse DFT of size 8 (per coordinate:
+    // the twiddles are base-field)
     const int br[8] = {0, 4, 2, 6, 1, 5, 3, 7};
 #pragma unroll
-    for (int k = 0; k < 8; k++) v[k] = layer_at(base, a.coset_major, a.logn, a.logbeta, i + (u64)br[k] * a.rows);
+    for (int k = 0; k < 8; k++) {
+        const u64 K = i + (u64)br[k] * a.rows;
+        v[k].a = layer_at(base, a.coset_major, a.logn, a.logbeta, K);
+        if constexpr (D == 2) v[k].b = layer_at(base + a.comp_stride, a.coset_major, a.logn, a.logbeta, K);
+    }
 #pragma unroll
     for (int s = 0; s < 3; s++) {
         const int h = 1 << s;
@@ -624,30 +703,35 @@ __global__ __launch_bounds__(256) void fri_fold_kernel(FoldArgs a) {
         for (int b = 0; b < 4; b++) {
             int pos = b & (h - 1), i0 = ((b >> s) << (s + 1)) + pos;
             u64 w = a.winv8[pos << (2 - s)];
-            u64 u = v[i0], t = gl_mul(v[i0 + h], w);
-            v[i0] = gl_add(u, t);
-            v[i0 + h] = gl_sub(u, t);
+            F u = v[i0], t = fe_mulb(v[i0 + h], w);
+            v[i0] = fe_add(u, t);
+            v[i0 + h] = fe_sub(u, t);
         }
     }
     // y = alpha * 7^-1 * w_D^-i ; Horner
-    u64 y = gl_mul(a.alpha7[proof], tw_ipow(a.T, a.logD, i));
-    u64 r = v[7];
+    const F y = fe_mulb(F::load(a.alpha7 + (u64)proof * D), tw_ipow(a.T, a.logD, i));
+    F r = v[7];
 #pragma unroll
-    for (int j = 6; j >= 0; j--) r = gl_add(gl_mul(r, y), v[j]);
-    a.out[(u64)proof * a.out_stride + i] = gl_mul(r, a.inv8);
+    for (int j = 6; j >= 0; j--) r = fe_add(fe_mul(r, y), v[j]);
+    r = fe_mulb(r, a.inv8);
+#pragma unroll
+    for (int c = 0; c < D; c++) a.out[((u64)proof * D + c) * a.out_stride + i] = r.c(c);
 }
-void launch_fri_fold(const u64* vals, u64 val_stride, bool coset_major, int logn, int logbeta, u64 rows, int logD,
-                     const u64* alpha7, u64* out, u64 out_stride, const Tables& T, int npoly, hipStream_t s) {
+void launch_fri_fold(const u64* vals, u64 val_stride, u64 comp_stride, bool coset_major, int logn, int logbeta,
+                     u64 rows, int logD, const u64* alpha7, u64* out, u64 out_stride, const Tables& T, int npoly,
+                     int ext, hipStream_t s) {
     FoldArgs a;
-    a.vals = vals; a.val_stride = val_stride; a.coset_major = coset_major ? 1 : 0; a.logn = logn;
-    a.logbeta = logbeta; a.rows = rows; a.logD = logD; a.alpha7 = alpha7; a.out = out; a.out_stride = out_stride;
+    a.vals = vals; a.val_stride = val_stride; a.comp_stride = comp_stride; a.coset_major = coset_major ? 1 : 0;
+    a.logn = logn; a.logbeta = logbeta; a.rows = rows; a.logD = logD; a.alpha7 = alpha7; a.out = out;
+    a.out_stride = out_stride;
     a.T = T;
     u64 w8inv = gl_inv(gl_root(3));
     for (int k = 0; k < 4; k++) a.winv8[k] = gl_pow(w8inv, k);
     a.inv8 = gl_inv(8);
     int threads = rows < 256 ? (int)rows : 256;
     dim3 g((unsigned)((rows + threads - 1) / threads), npoly);
-    hipLaunchKernelGGL(fri_fold_kernel, g, dim3(threads), 0, s, a);
+    if (ext == 2) hipLaunchKernelGGL(fri_fold_kernel<2>, g, dim3(threads), 0, s, a);
+    else hipLaunchKernelGGL(fri_fold_kernel<1>, g, dim3(threads), 0, s, a);
     XFG_CHECK_LAUNCH();
 }
 

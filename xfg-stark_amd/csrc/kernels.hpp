@@ -15,14 +15,15 @@ struct AirConst {
     u64 pad[2];
 };
 
-// per-proof DEEP parameters: trace coefficients a_i, composition coefficient, OOD points and the
+// per-proof DEEP parameters, every value an element of E (2 coordinates; the second is 0 without
+// a field extension): trace coefficients a_i, composition coefficient, OOD points and the
 // constant terms c1 = sum a_i T_i(z) + gamma H(z), c2 = sum a_i T_i(z g)
 struct DeepParams {
-    u64 a[7];
-    u64 gamma;
-    u64 z, zg, zinv, zginv;
-    u64 c1, c2;
-    u64 pad[4];
+    u64 a[7][2];
+    u64 gamma[2];
+    u64 z[2], zg[2], zinv[2], zginv[2];
+    u64 c1[2], c2[2];
+    u64 pad[2];
 };
 
 struct Tables {
@@ -54,8 +55,8 @@ void launch_open_rows(const u64* lde, int nc, const u64* entries, u64 count, Dig
 // FRI layer leaves: row i = values at natural indices i + k*rows, k < 8 (coset-major source when
 // coset_major, else natural); all leaves stored at nodes[rows + i]
 // (returns the node count left for launch_tree_top, like launch_leaves_lde)
-u64 launch_fri_leaves(const u64* vals, u64 val_stride, bool coset_major, int logn, int logbeta, u64 rows,
-                      Digest* nodes, u64 node_stride, int npoly, hipStream_t s);
+u64 launch_fri_leaves(const u64* vals, u64 val_stride, u64 comp_stride, bool coset_major, int logn, int logbeta,
+                      u64 rows, Digest* nodes, u64 node_stride, int npoly, int ext, hipStream_t s);
 // completes the tree above level `count` (nodes [count, 2count) present) up to the root
 void launch_tree_top(Digest* nodes, u64 node_stride, u64 count, int npoly, hipStream_t s);
 
@@ -63,22 +64,25 @@ void launch_tree_top(Digest* nodes, u64 node_stride, u64 count, int npoly, hipSt
 void launch_trace_gen(const AirConst* air, u64* trace, int logn, int npoly, hipStream_t s);
 // composition evaluations over the CE domain 7*<w_2n> (natural order) from the trace LDE
 // div = constraint divisor table [3][2][n] from ce_divisor_table()
-void launch_constraint_eval(const u64* lde, const AirConst* air, const u64* coeffs /*[B][15]*/, const u64* div,
-                            u64* ce, int logn, int logbeta, int npoly, hipStream_t s);
+// ext = extension degree D: coeffs [B][15][D], ce planes [B][D][2n]
+void launch_constraint_eval(const u64* lde, const AirConst* air, const u64* coeffs, const u64* div, u64* ce, int logn,
+                            int logbeta, int npoly, int ext, hipStream_t s);
 
 // ---- OOD / DEEP ----
 // partial: [B][ood_partial_count(logn)][15] per-block sums, kept for launch_deep
-void launch_ood(const u64* coef, const u64* hcoef, const u64* zpts /*[B][2]*/, u64* partial, u64* ood /*[B][15]*/,
-                int logn, int npoly, hipStream_t s);
+// ext = D: zpts [B][2][D], hcoef planes [B][D][n], partial [B][count][15][D], ood [B][15][D]
+void launch_ood(const u64* coef, const u64* hcoef, const u64* zpts, u64* partial, u64* ood, int logn, int npoly,
+                int ext, hipStream_t s);
 u64 ood_partial_count(int logn);
-// carry: [B][ood_partial_count(logn)][2]
+// carry: [B][ood_partial_count(logn)][2][D]; deep planes [B][D][n]
 void launch_deep(const u64* coef, const u64* hcoef, const DeepParams* dp, const u64* partial, u64* carry, u64* deep,
-                 int logn, int npoly, hipStream_t s);
+                 int logn, int npoly, int ext, hipStream_t s);
 
 // ---- FRI ----
-void launch_fri_fold(const u64* vals, u64 val_stride, bool coset_major, int logn, int logbeta, u64 rows, int logD,
-                     const u64* alpha7 /*[B] = alpha * 7^-1*/, u64* out, u64 out_stride, const Tables& T, int npoly,
-                     hipStream_t s);
+// alpha7 [B][D] = alpha * 7^-1; E values as D planes comp_stride apart; out planes [B][D][out_stride]
+void launch_fri_fold(const u64* vals, u64 val_stride, u64 comp_stride, bool coset_major, int logn, int logbeta,
+                     u64 rows, int logD, const u64* alpha7, u64* out, u64 out_stride, const Tables& T, int npoly,
+                     int ext, hipStream_t s);
 
 // ---- openings ----
 void launch_gather_u64(const u64* src, const u64* idx, u64* dst, u64 count, hipStream_t s);

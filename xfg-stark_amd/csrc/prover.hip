@@ -362,7 +362,8 @@ struct ProofJob {
     AirConst air;
     Coin coin;
     std::vector<uint8_t> commitments;
-    u64 ood[15];
+    u64 ood[30];           // 15 E elements ([T_c(z), T_c(zg)] x 7, H(z)), DE coordinates each
+    std::vector<u64> rem;  // FRI remainder, E elements
     u64 nonce = 0;
     std::vector<u64> pos;
     std::vector<uint8_t> bytes;
@@ -428,29 +429,30 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     const int logn = (int)ilog2(n), logbeta = (int)ilog2(o.beta);
     const u64 beta = o.beta, N = n * beta;
     const unsigned nl = num_fri_layers(N, o);
+    const int DE = (int)o.ext;  // extension degree: E-valued data is DE coordinate planes
     hipStream_t s = c->stream;
 
     // ---- buffers
     c->air.ensure(B);
-    c->coeffs.ensure((size_t)B * 15);
+    c->coeffs.ensure((size_t)B * 15 * DE);
     c->trace.ensure((size_t)B * 7 * n);
     c->coef.ensure((size_t)B * 7 * n);
     c->scratch.ensure((size_t)B * 7 * N);
     c->lde.ensure((size_t)B * 7 * N);
     c->tnodes.ensure((size_t)B * 2 * n);
-    c->ce.ensure((size_t)B * 2 * n);
-    c->hcoef.ensure((size_t)B * n);
-    c->hlde.ensure((size_t)B * N);
+    c->ce.ensure((size_t)B * DE * 2 * n);
+    c->hcoef.ensure((size_t)B * DE * n);
+    c->hlde.ensure((size_t)B * DE * N);
     c->hnodes.ensure((size_t)B * 2 * n);
-    c->zpts.ensure((size_t)B * 2);
-    c->partial.ensure((size_t)B * 15 * ood_partial_count(logn));
-    c->ood.ensure((size_t)B * 15);
+    c->zpts.ensure((size_t)B * 2 * DE);
+    c->partial.ensure((size_t)B * 15 * DE * ood_partial_count(logn));
+    c->ood.ensure((size_t)B * 15 * DE);
     c->dp.ensure(B);
-    c->carry.ensure((size_t)B * 2 * ood_partial_count(logn));
-    c->deep.ensure((size_t)B * n);
-    c->f0.ensure((size_t)B * N);
-    c->alpha7.ensure(B);
-    c->dn2.ensure(B);
+    c->carry.ensure((size_t)B * 2 * DE * ood_partial_count(logn));
+    c->deep.ensure((size_t)B * DE * n);
+    c->f0.ensure((size_t)B * DE * N);
+    c->alpha7.ensure((size_t)B * DE);
+    c->dn2.ensure((size_t)B * DE);
     if (c->flayer.size() < nl + 1) {
         c->flayer.resize(nl + 1);
         c->fnodes.resize(nl + 1);
@@ -460,15 +462,15 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     for (unsigned l = 1; l <= nl; l++) D[l] = D[l - 1] / o.fold;
     for (unsigned l = 0; l < nl; l++) {
         c->fnodes[l].ensure((size_t)B * 2 * (D[l] / o.fold));
-        c->flayer[l + 1].ensure((size_t)B * D[l + 1]);
+        c->flayer[l + 1].ensure((size_t)B * DE * D[l + 1]);
     }
     const u64 rem_len = N >> (3 * nl) >> logbeta;  // D_final / blowup
-    c->rem.ensure((size_t)B * std::max<u64>(rem_len, 1));
+    c->rem.ensure((size_t)B * DE * std::max<u64>(rem_len, 1));
     {
         // opening buffers sized by upper bounds once, so steady-state calls never re-allocate
         // (hipFree / hipHostMalloc would serialise the device and the other lanes)
         const size_t q = o.q, depth = logn + logbeta;
-        const size_t vals = (size_t)B * q * (8 + 8 * nl);
+        const size_t vals = (size_t)B * q * (7 + DE + 8 * DE * nl);
         size_t digs = (size_t)B * q * 2 * depth;
         for (unsigned l = 0; l < nl; l++) digs += (size_t)B * q * ilog2(D[l] / 8);
         const size_t opens = (size_t)B * q * 2 * 2 * 2 * beta;
@@ -509,7 +511,7 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     ht.mark("sync_trace_root");
 
     // ---- 2. constraint composition coefficients (7 transition + 8 boundary)
-    u64* co = c->h_co.ensure((size_t)B * 15);
+    u64* co = c->h_co.ensure((size_t)B * 15 * DE);
     for (int b = 0; b < B; b++) {
         auto& j = jobs[b];
         uint8_t rb[32];
@@ -517,17 +519,17 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         j.commitments.insert(j.commitments.end(), rb, rb + 32);
         j.coin.reseed(roots[b]);
         for (int k = 0; k < 15; k++)
-            if (!j.coin.draw(co[(size_t)b * 15 + k])) j.status = XFG_PROVER_ERROR;
+            if (!j.coin.draw_e(co + ((size_t)b * 15 + k) * DE, DE)) j.status = XFG_PROVER_ERROR;
     }
-    HIPCHK(hipMemcpyAsync(c->coeffs.p, co, (size_t)B * 15 * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->coeffs.p, co, (size_t)B * 15 * DE * 8, hipMemcpyHostToDevice, s));
 
     // ---- 3. constraint evaluation + composition polynomial + commitment
-    launch_constraint_eval(c->lde.p, c->air.p, c->coeffs.p, ce_div, c->ce.p, logn, logbeta, B, s);
+    launch_constraint_eval(c->lde.p, c->air.p, c->coeffs.p, ce_div, c->ce.p, logn, logbeta, B, DE, s);
     stage_mark(c, 3);
-    launch_interpolate(c->ce.p, 2 * n, c->hcoef.p, n, c->scratch.p, B, logn + 1, true, n, T, s);
-    launch_lde(c->hcoef.p, n, c->hlde.p, c->scratch.p, B, logn, logbeta, T, s);
+    launch_interpolate(c->ce.p, 2 * n, c->hcoef.p, n, c->scratch.p, B * DE, logn + 1, true, n, T, s);
+    launch_lde(c->hcoef.p, n, c->hlde.p, c->scratch.p, B * DE, logn, logbeta, T, s);
     stage_mark(c, 4);
-    launch_tree_top(c->hnodes.p, 2 * n, launch_leaves_lde(c->hlde.p, 1, c->hnodes.p, 2 * n, B, logn, logbeta, s), B,
+    launch_tree_top(c->hnodes.p, 2 * n, launch_leaves_lde(c->hlde.p, DE, c->hnodes.p, 2 * n, B, logn, logbeta, s), B,
                     s);
     stage_mark(c, 5);
     ht.mark("launch2");
@@ -536,22 +538,24 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
 
     // ---- 4. OOD point and frame
     const u64 g = gl_root(logn);
-    u64* zp = c->h_zp.ensure((size_t)B * 2);
+    u64* zp = c->h_zp.ensure((size_t)B * 2 * DE);  // [b][z, z g][DE]
     for (int b = 0; b < B; b++) {
         auto& j = jobs[b];
         uint8_t rb[32];
         digest_bytes(roots[b], rb);
         j.commitments.insert(j.commitments.end(), rb, rb + 32);
         j.coin.reseed(roots[b]);
-        u64 z = 0;
-        if (!j.coin.draw(z)) j.status = XFG_PROVER_ERROR;
-        zp[2 * b] = z;
-        zp[2 * b + 1] = gl_mul(z, g);
+        u64 z[2] = {0, 0};
+        if (!j.coin.draw_e(z, DE)) j.status = XFG_PROVER_ERROR;
+        for (int k = 0; k < DE; k++) {
+            zp[(size_t)b * 2 * DE + k] = z[k];
+            zp[(size_t)b * 2 * DE + DE + k] = gl_mul(z[k], g);
+        }
     }
-    HIPCHK(hipMemcpyAsync(c->zpts.p, zp, (size_t)B * 2 * 8, hipMemcpyHostToDevice, s));
-    launch_ood(c->coef.p, c->hcoef.p, c->zpts.p, c->partial.p, c->ood.p, logn, B, s);
-    u64* ood = c->h_ood.ensure((size_t)B * 15);
-    HIPCHK(hipMemcpyAsync(ood, c->ood.p, (size_t)B * 15 * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(c->zpts.p, zp, (size_t)B * 2 * DE * 8, hipMemcpyHostToDevice, s));
+    launch_ood(c->coef.p, c->hcoef.p, c->zpts.p, c->partial.p, c->ood.p, logn, B, DE, s);
+    u64* ood = c->h_ood.ensure((size_t)B * 15 * DE);
+    HIPCHK(hipMemcpyAsync(ood, c->ood.p, (size_t)B * 15 * DE * 8, hipMemcpyDeviceToHost, s));
     stage_mark(c, 6);
     ht.mark("launch3");
     HIPCHK(hipStreamSynchronize(s));
@@ -561,43 +565,50 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     DeepParams* dps = c->h_dp.ensure(B);
     for (int b = 0; b < B; b++) {
         auto& j = jobs[b];
-        memcpy(j.ood, &ood[(size_t)b * 15], 15 * 8);
-        j.coin.reseed(hash_elements(j.ood, 14));  // interleaved T_i(z), T_i(zg)
-        j.coin.reseed(hash_elements(j.ood + 14, 1));
+        memcpy(j.ood, &ood[(size_t)b * 15 * DE], 15 * DE * 8);  // [15][DE]
+        j.coin.reseed(hash_elements(j.ood, 14 * DE));  // interleaved T_i(z), T_i(zg), E elements
+        j.coin.reseed(hash_elements(j.ood + 14 * DE, DE));
         DeepParams& P = dps[b];
         memset(&P, 0, sizeof P);
         for (int k = 0; k < 7; k++)
-            if (!j.coin.draw(P.a[k])) j.status = XFG_PROVER_ERROR;
-        if (!j.coin.draw(P.gamma)) j.status = XFG_PROVER_ERROR;
-        P.z = zp[2 * b];
-        P.zg = zp[2 * b + 1];
-        if (P.z == 0 || P.zg == 0) j.status = XFG_PROVER_ERROR;
-        P.zinv = P.z ? gl_inv(P.z) : 0;
-        P.zginv = P.zg ? gl_inv(P.zg) : 0;
-        u64 c1 = gl_mul(P.gamma, j.ood[14]), c2 = 0;
+            if (!j.coin.draw_e(P.a[k], DE)) j.status = XFG_PROVER_ERROR;
+        if (!j.coin.draw_e(P.gamma, DE)) j.status = XFG_PROVER_ERROR;
+        const u64* zb = zp + (size_t)b * 2 * DE;
+        const E2 z{zb[0], DE == 2 ? zb[1] : 0}, zg{zb[DE], DE == 2 ? zb[DE + 1] : 0};
+        if ((z.a == 0 && z.b == 0) || (zg.a == 0 && zg.b == 0)) j.status = XFG_PROVER_ERROR;
+        const E2 zi = (z.a || z.b) ? e2_inv(z) : E2{0, 0}, zgi = (zg.a || zg.b) ? e2_inv(zg) : E2{0, 0};
+        auto put = [](u64* d, E2 v) { d[0] = v.a; d[1] = v.b; };
+        auto ood_e = [&](int q) { return E2{j.ood[q * DE], DE == 2 ? j.ood[q * DE + 1] : 0}; };
+        put(P.z, z);
+        put(P.zg, zg);
+        put(P.zinv, zi);
+        put(P.zginv, zgi);
+        E2 c1 = e2_mul(E2{P.gamma[0], P.gamma[1]}, ood_e(14)), c2{0, 0};
         for (int k = 0; k < 7; k++) {
-            c1 = gl_add(c1, gl_mul(P.a[k], j.ood[2 * k]));
-            c2 = gl_add(c2, gl_mul(P.a[k], j.ood[2 * k + 1]));
+            const E2 a{P.a[k][0], P.a[k][1]};
+            c1 = e2_add(c1, e2_mul(a, ood_e(2 * k)));
+            c2 = e2_add(c2, e2_mul(a, ood_e(2 * k + 1)));
         }
-        P.c1 = c1;
-        P.c2 = c2;
+        put(P.c1, c1);
+        put(P.c2, c2);
     }
     HIPCHK(hipMemcpyAsync(c->dp.p, dps, B * sizeof(DeepParams), hipMemcpyHostToDevice, s));
-    launch_deep(c->coef.p, c->hcoef.p, c->dp.p, c->partial.p, c->carry.p, c->deep.p, logn, B, s);
-    launch_lde(c->deep.p, n, c->f0.p, c->scratch.p, B, logn, logbeta, T, s);
+    launch_deep(c->coef.p, c->hcoef.p, c->dp.p, c->partial.p, c->carry.p, c->deep.p, logn, B, DE, s);
+    launch_lde(c->deep.p, n, c->f0.p, c->scratch.p, B * DE, logn, logbeta, T, s);
     // degree check: deg(DEEP) == n - 2  <=>  coefficient n-2 != 0 (coefficient n-1 is 0 by construction)
-    HIPCHK(hipMemcpy2DAsync(c->dn2.p, 8, c->deep.p + (n - 2), n * 8, 8, B, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpy2DAsync(c->dn2.p, 8, c->deep.p + (n - 2), n * 8, 8, (size_t)B * DE, hipMemcpyDeviceToDevice, s));
     stage_mark(c, 7);
 
     // ---- 6. FRI layers (FriProver::build_layers), folding factor 8
-    u64* alpha7h = c->h_a7.ensure(B);
+    u64* alpha7h = c->h_a7.ensure((size_t)B * DE);
     const u64 inv7 = gl_inv(GEN);
     for (unsigned l = 0; l < nl; l++) {
         const u64 rows = D[l] / 8;
         const bool cm = (l == 0);
         const u64* src = cm ? c->f0.p : c->flayer[l].p;
-        const u64 sstride = cm ? N : D[l];
-        u64 top = launch_fri_leaves(src, sstride, cm, logn, logbeta, rows, c->fnodes[l].p, 2 * rows, B, s);
+        const u64 cstride = cm ? N : D[l], sstride = DE * cstride;
+        u64 top = launch_fri_leaves(src, sstride, cstride, cm, logn, logbeta, rows, c->fnodes[l].p, 2 * rows, B, DE,
+                                    s);
         launch_tree_top(c->fnodes[l].p, 2 * rows, top, B, s);
         ht.mark("fri_launch");
         fetch_roots(c, c->fnodes[l].p, 2 * rows, B, roots);
@@ -608,26 +619,27 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
             digest_bytes(roots[b], rb);
             j.commitments.insert(j.commitments.end(), rb, rb + 32);
             j.coin.reseed(roots[b]);
-            u64 a = 0;
-            if (!j.coin.draw(a)) j.status = XFG_PROVER_ERROR;
-            alpha7h[b] = gl_mul(a, inv7);
+            u64 a[2] = {0, 0};
+            if (!j.coin.draw_e(a, DE)) j.status = XFG_PROVER_ERROR;
+            for (int k = 0; k < DE; k++) alpha7h[(size_t)b * DE + k] = gl_mul(a[k], inv7);
         }
-        HIPCHK(hipMemcpyAsync(c->alpha7.p, alpha7h, B * 8, hipMemcpyHostToDevice, s));
-        launch_fri_fold(src, sstride, cm, logn, logbeta, rows, (int)ilog2(D[l]), c->alpha7.p, c->flayer[l + 1].p,
-                        rows, T, B, s);
+        HIPCHK(hipMemcpyAsync(c->alpha7.p, alpha7h, (size_t)B * DE * 8, hipMemcpyHostToDevice, s));
+        launch_fri_fold(src, sstride, cstride, cm, logn, logbeta, rows, (int)ilog2(D[l]), c->alpha7.p,
+                        c->flayer[l + 1].p, rows, T, B, DE, s);
     }
     // remainder: interpolate the last layer over 7*<w_D>, keep D/blowup coefficients
     // (with no folding layer this is the DEEP polynomial's own coefficients)
-    u64* remh = c->h_rem.ensure((size_t)B * rem_len);
+    u64* remh = c->h_rem.ensure((size_t)B * DE * rem_len);  // planes [b][c][rem_len]
     if (nl > 0) {
-        launch_interpolate(c->flayer[nl].p, D[nl], c->rem.p, rem_len, c->scratch.p, B, (int)ilog2(D[nl]), true,
+        launch_interpolate(c->flayer[nl].p, D[nl], c->rem.p, rem_len, c->scratch.p, B * DE, (int)ilog2(D[nl]), true,
                            rem_len, T, s);
-        HIPCHK(hipMemcpyAsync(remh, c->rem.p, (size_t)B * rem_len * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(remh, c->rem.p, (size_t)B * DE * rem_len * 8, hipMemcpyDeviceToHost, s));
     } else {
-        HIPCHK(hipMemcpy2DAsync(remh, rem_len * 8, c->deep.p, n * 8, rem_len * 8, B, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpy2DAsync(remh, rem_len * 8, c->deep.p, n * 8, rem_len * 8, (size_t)B * DE, hipMemcpyDeviceToHost,
+                                s));
     }
-    u64* dn2h = c->h_dn2.ensure(B);
-    HIPCHK(hipMemcpyAsync(dn2h, c->dn2.p, B * 8, hipMemcpyDeviceToHost, s));
+    u64* dn2h = c->h_dn2.ensure((size_t)B * DE);
+    HIPCHK(hipMemcpyAsync(dn2h, c->dn2.p, (size_t)B * DE * 8, hipMemcpyDeviceToHost, s));
     stage_mark(c, 8);
     ht.mark("launch_rem");
     HIPCHK(hipStreamSynchronize(s));
@@ -650,8 +662,12 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     for (int b = 0; b < B; b++) {
         auto& j = jobs[b];
         ht.tic();
-        if (dn2h[b] == 0) j.status = XFG_PROVER_ERROR;  // assert_eq!(trace_length - 2, degree)
-        Digest rc = hash_elements(&remh[(size_t)b * rem_len], rem_len);
+        if (dn2h[(size_t)b * DE] == 0 && dn2h[(size_t)b * DE + DE - 1] == 0)
+            j.status = XFG_PROVER_ERROR;  // assert_eq!(trace_length - 2, degree)
+        j.rem.resize(rem_len * DE);  // E elements, coordinates interleaved
+        for (u64 i = 0; i < rem_len; i++)
+            for (int k = 0; k < DE; k++) j.rem[i * DE + k] = remh[((size_t)b * DE + k) * rem_len + i];
+        Digest rc = hash_elements(j.rem.data(), rem_len * DE);
         uint8_t rb[32];
         digest_bytes(rc, rb);
         j.commitments.insert(j.commitments.end(), rb, rb + 32);
@@ -675,7 +691,7 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         for (u64 k : pos) {
             u64 t = k & (beta - 1), m = k >> logbeta;
             for (int col = 0; col < 7; col++) vidx_lde.push_back((((u64)b * 7 + col) * beta + t) * n + m);
-            vidx_h.push_back(((u64)b * beta + t) * n + m);
+            for (int k = 0; k < DE; k++) vidx_h.push_back((((u64)b * DE + k) * beta + t) * n + m);
         }
         // rows whose subtrees are recomputed: every queried row and its sibling row (the sibling's
         // subtree top, heap level log2(beta), is no longer stored)
@@ -711,9 +727,13 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
             L.fpos.push_back(fp);
             for (u64 i : fp)
                 for (u64 k = 0; k < 8; k++) {
-                    u64 K = i + k * rows;
-                    if (l == 0) vidx_f[0].push_back(((u64)b * beta + (K & (beta - 1))) * n + (K >> logbeta));
-                    else vidx_f[l].push_back((u64)b * D[l] + K);
+                    const u64 K = i + k * rows;
+                    for (int cc = 0; cc < DE; cc++) {
+                        if (l == 0)
+                            vidx_f[0].push_back((((u64)b * DE + cc) * beta + (K & (beta - 1))) * n + (K >> logbeta));
+                        else
+                            vidx_f[l].push_back(((u64)b * DE + cc) * D[l] + K);
+                    }
                 }
             L.fops.emplace_back();
             plan_batch_opening(fp, rows, L.fops.back());
@@ -761,7 +781,7 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         }
         const u64* ent = c->gidx.p + nvals + ndig;
         launch_open_rows(c->lde.p, 7, ent, nent, c->gdig.p + ndig, logn, logbeta, s);
-        launch_open_rows(c->hlde.p, 1, ent, nent, c->gdig.p + ndig + nopen, logn, logbeta, s);
+        launch_open_rows(c->hlde.p, DE, ent, nent, c->gdig.p + ndig + nopen, logn, logbeta, s);
     }
     u64* gv = c->h_gv.ensure(nvals);
     Digest* gd = c->h_gd.ensure(ndig + 2 * nopen);
@@ -814,7 +834,8 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         auto& j = jobs[b];
         const u64 nu = j.pos.size();
         BW w;
-        w.b.resize(j.commitments.size() + nu * 8 * (8 + 8 * nl) + (2 + nl) * nu * 32 * ilog2(N) + 1024);
+        w.b.resize(j.commitments.size() + nu * 8 * (7 + DE + 8 * DE * nl) + (2 + nl) * nu * 32 * ilog2(N) +
+                   rem_len * 8 * DE + 1024);
         // Context
         w.u8(7); w.u8(0); w.u8(logn); w.u16(0);
         w.u8(8); w.u64_(P);
@@ -829,27 +850,27 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         cur_lde += nu * 7;
         write_lde_paths(w, lay[b], cur_t, open_t);
         // constraint queries
-        w.u32(nu * 8);
-        w.u64s(&gv[cur_h], nu);
-        cur_h += nu;
+        w.u32(nu * 8 * DE);
+        w.u64s(&gv[cur_h], nu * DE);
+        cur_h += nu * DE;
         write_lde_paths(w, lay[b], cur_hd, open_h);
-        // OOD frame
-        w.u16(1 + 14 * 8);
+        // OOD frame (E elements)
+        w.u16(1 + 14 * 8 * DE);
         w.u8(2);
-        for (int k = 0; k < 14; k++) w.u64_(j.ood[k]);
-        w.u16(8);
-        w.u64_(j.ood[14]);
+        w.u64s(j.ood, 14 * DE);
+        w.u16(8 * DE);
+        w.u64s(j.ood + 14 * DE, DE);
         // FRI proof
         w.u8(nl);
         for (unsigned l = 0; l < nl; l++) {
             u64 nk = lay[b].fpos[l].size();
-            w.u32(nk * 8 * 8);
-            w.u64s(&gv[cur_fv[l]], nk * 8);
-            cur_fv[l] += nk * 8;
+            w.u32(nk * 8 * 8 * DE);
+            w.u64s(&gv[cur_fv[l]], nk * 8 * DE);
+            cur_fv[l] += nk * 8 * DE;
             write_paths(w, lay[b].fops[l], cur_fd[l]);
         }
-        w.u16(rem_len * 8);
-        for (u64 i = 0; i < rem_len; i++) w.u64_(remh[(size_t)b * rem_len + i]);
+        w.u16(rem_len * 8 * DE);
+        w.u64s(j.rem.data(), rem_len * DE);
         w.u8(0);
         w.u64_(j.nonce);
         w.finish(j.bytes);
@@ -1147,9 +1168,10 @@ size_t xfg_proof_size_bound(uint64_t n, const xfg_options* opts) {
     Opts o = to_opts(opts);
     u64 N = n * o.beta, depth = ilog2(N);
     unsigned L = num_fri_layers(N, o);
-    size_t s = 4096 + o.q * (7 * 8 + 8 + (size_t)L * o.fold * 8);
+    const size_t de = o.ext == 2 ? 2 : 1;
+    size_t s = 4096 + o.q * (7 * 8 + 8 * de + (size_t)L * o.fold * 8 * de);
     s += (size_t)(2 + L) * (1 + o.q * (1 + depth * 32));
-    s += (size_t)N * 8 / o.beta + 32 * (L + 3);
+    s += (size_t)N * 8 * de / o.beta + 32 * (L + 3);
     return s;
 }
 
@@ -1488,30 +1510,30 @@ int xfg_debug_ood_deep(xfg_ctx* c, uint32_t count, uint64_t n, const uint64_t* c
         HIPCHK(hipMemcpyAsync(L->coef.p, coef, B * 7 * n * 8, hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(L->hcoef.p, hcoef, B * n * 8, hipMemcpyHostToDevice, s));
         HIPCHK(hipMemcpyAsync(L->zpts.p, zpts, B * 2 * 8, hipMemcpyHostToDevice, s));
-        launch_ood(L->coef.p, L->hcoef.p, L->zpts.p, L->partial.p, L->ood.p, logn, (int)B, s);
+        launch_ood(L->coef.p, L->hcoef.p, L->zpts.p, L->partial.p, L->ood.p, logn, (int)B, 1, s);
         HIPCHK(hipMemcpyAsync(ood_out, L->ood.p, B * 15 * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         std::vector<DeepParams> dps(B);
         for (size_t b = 0; b < B; b++) {  // as prove_lane: c1, c2 from the OOD values
             DeepParams& P = dps[b];
             memset(&P, 0, sizeof P);
-            memcpy(P.a, coeffs + b * 8, 7 * 8);
-            P.gamma = coeffs[b * 8 + 7];
-            P.z = zpts[2 * b];
-            P.zg = zpts[2 * b + 1];
-            P.zinv = gl_inv(P.z);
-            P.zginv = gl_inv(P.zg);
+            for (int k = 0; k < 7; k++) P.a[k][0] = coeffs[b * 8 + k];
+            P.gamma[0] = coeffs[b * 8 + 7];
+            P.z[0] = zpts[2 * b];
+            P.zg[0] = zpts[2 * b + 1];
+            P.zinv[0] = gl_inv(P.z[0]);
+            P.zginv[0] = gl_inv(P.zg[0]);
             const u64* o = ood_out + b * 15;
-            u64 c1 = gl_mul(P.gamma, o[14]), c2 = 0;
+            u64 c1 = gl_mul(P.gamma[0], o[14]), c2 = 0;
             for (int k = 0; k < 7; k++) {
-                c1 = gl_add(c1, gl_mul(P.a[k], o[2 * k]));
-                c2 = gl_add(c2, gl_mul(P.a[k], o[2 * k + 1]));
+                c1 = gl_add(c1, gl_mul(P.a[k][0], o[2 * k]));
+                c2 = gl_add(c2, gl_mul(P.a[k][0], o[2 * k + 1]));
             }
-            P.c1 = c1;
-            P.c2 = c2;
+            P.c1[0] = c1;
+            P.c2[0] = c2;
         }
         HIPCHK(hipMemcpyAsync(L->dp.p, dps.data(), B * sizeof(DeepParams), hipMemcpyHostToDevice, s));
-        launch_deep(L->coef.p, L->hcoef.p, L->dp.p, L->partial.p, L->carry.p, L->deep.p, logn, (int)B, s);
+        launch_deep(L->coef.p, L->hcoef.p, L->dp.p, L->partial.p, L->carry.p, L->deep.p, logn, (int)B, 1, s);
         HIPCHK(hipMemcpyAsync(deep_out, L->deep.p, B * n * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         return XFG_OK;

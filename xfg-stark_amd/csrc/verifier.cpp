@@ -62,7 +62,7 @@ struct ParsedProof {
     std::vector<Digest> com;  // trace root, constraint root, FRI layer roots, remainder commitment
     Span trace_rows, constraint_rows, ood, fri_rem;
     Paths trace_paths, constraint_paths;
-    u64 hz = 0;
+    Span hz;
     std::vector<Span> fri_vals;
     std::vector<Paths> fri_paths;
     u64 partitions = 0, nonce = 0;
@@ -124,11 +124,12 @@ static std::string parse_proof(const uint8_t* bytes, size_t len, ParsedProof& pf
         return "ProofDeserializationError(\"constraint query paths\")";
     Span hz;
     if (!read_span(r, 2, pf.ood) || !read_span(r, 2, hz)) return "ProofDeserializationError(\"OOD frame\")";
-    if (pf.ood.n < 1 || pf.ood.p[0] != 2 || (pf.ood.n - 1) % 16 || hz.n != 8)
+    const size_t esz = pf.o.ext == 2 ? 16 : 8;  // bytes per E element
+    if (pf.ood.n < 1 || pf.ood.p[0] != 2 || (pf.ood.n - 1) % (2 * esz) || hz.n != esz)
         return "ProofDeserializationError(\"OOD frame layout\")";
     pf.ood.p += 1;
     pf.ood.n -= 1;
-    pf.hz = hz.elem(0);
+    pf.hz = hz;
     const u64 nl = r.u(1);
     pf.fri_vals.resize(nl);
     pf.fri_paths.resize(nl);
@@ -137,7 +138,7 @@ static std::string parse_proof(const uint8_t* bytes, size_t len, ParsedProof& pf
         const u64 pl = r.u(4);
         if (r.bad || !read_paths(r, pl, pf.fri_paths[l])) return "ProofDeserializationError(\"FRI layer paths\")";
     }
-    if (!read_span(r, 2, pf.fri_rem) || pf.fri_rem.n % 8) return "ProofDeserializationError(\"FRI remainder\")";
+    if (!read_span(r, 2, pf.fri_rem) || pf.fri_rem.n % esz) return "ProofDeserializationError(\"FRI remainder\")";
     pf.partitions = r.u(1);
     pf.nonce = r.u(8);
     if (r.bad) return "ProofDeserializationError(\"unexpected end of input\")";
@@ -186,38 +187,40 @@ static Digest leaf_hash(const uint8_t* bytes, size_t len) { return blake3_bytes(
 // ------------------------------------------------------------------ burn AIR at a point
 // evaluate_transition (src/burn_mint_air.rs:335-378, corrected AIR A.2) and the 8 assertions
 // (:380-395, final state assertion at n - 1)
-static void air_transition(const AirConst& a, const u64 cur[7], const u64 nxt[7], u64 r[7]) {
+// evaluated over E (the OOD frame is E-valued with a field extension; base values have b = 0)
+static void air_transition(const AirConst& a, const E2 cur[7], const E2 nxt[7], E2 r[7]) {
     const u64 std_burn = 8000000ULL, large = gl_mul(std_burn, 1000);
-    r[0] = gl_mul(gl_sub(cur[0], std_burn), gl_sub(cur[0], large));
-    r[1] = gl_sub(cur[1], cur[0]);
-    r[2] = gl_sub(cur[2], a.pub[2]);
-    r[3] = gl_sub(cur[3], a.pub[3]);
-    const u64 d = gl_sub(nxt[4], cur[4]);
-    r[4] = gl_mul(d, gl_sub(d, 1));
-    r[5] = gl_sub(cur[5], a.nullifier);
-    r[6] = gl_sub(cur[6], a.commitment);
+    r[0] = e2_mul(e2_sub(cur[0], e2(std_burn)), e2_sub(cur[0], e2(large)));
+    r[1] = e2_sub(cur[1], cur[0]);
+    r[2] = e2_sub(cur[2], e2(a.pub[2]));
+    r[3] = e2_sub(cur[3], e2(a.pub[3]));
+    const E2 d = e2_sub(nxt[4], cur[4]);
+    r[4] = e2_mul(d, e2_sub(d, e2(1)));
+    r[5] = e2_sub(cur[5], e2(a.nullifier));
+    r[6] = e2_sub(cur[6], e2(a.commitment));
 }
 
 // FRI apply_drp on one row (folding 8, domain offset 7): interpolate the 8 values on the coset
-// x * <w_8> and evaluate at alpha
-static u64 fold_row(const u64 v[8], u64 x, u64 alpha) {
-    // coefficients of the degree < 8 interpolant in (X / x): c = iDFT_8(v) / 8
-    const u64 w8 = gl_root(3);
-    u64 c[8];
-    u64 winv = gl_inv(w8), inv8 = gl_inv(8);
+// x * <w_8> (per coordinate: base-field weights) and evaluate at alpha
+static E2 fold_row(const E2 v[8], u64 x, E2 alpha) {
+    const u64 winv = gl_inv(gl_root(3)), inv8 = gl_inv(8);
+    E2 c[8];
     for (int k = 0; k < 8; k++) {
-        u64 s = 0, wk = gl_pow(winv, (u64)k), p = 1;
+        E2 s{0, 0};
+        u64 wk = gl_pow(winv, (u64)k), p = 1;
         for (int j = 0; j < 8; j++) {
-            s = gl_add(s, gl_mul(v[j], p));
+            s = e2_add(s, e2_mulb(v[j], p));
             p = gl_mul(p, wk);
         }
-        c[k] = gl_mul(s, inv8);
+        c[k] = e2_mulb(s, inv8);
     }
-    const u64 t = gl_mul(alpha, gl_inv(x));
-    u64 r = 0;
-    for (int k = 7; k >= 0; k--) r = gl_add(gl_mul(r, t), c[k]);
+    const E2 t = e2_mulb(alpha, gl_inv(x));
+    E2 r{0, 0};
+    for (int k = 7; k >= 0; k--) r = e2_add(e2_mul(r, t), c[k]);
     return r;
 }
+// E element i of a span of DE-coordinate elements
+static E2 elem_e(const Span& s, size_t i, int de) { return de == 2 ? E2{s.elem(2 * i), s.elem(2 * i + 1)} : e2(s.elem(i)); }
 
 // returns "" when the proof verifies, else the VerifierError (Debug form)
 static std::string verify_proof(const uint8_t* bytes, size_t len, const AirConst& air, const Opts& acceptable) {
@@ -229,14 +232,21 @@ static std::string verify_proof(const uint8_t* bytes, size_t len, const AirConst
     if (memcmp(&o, &acceptable, sizeof o)) return "UnacceptableProofOptions";  // AcceptableOptions::OptionSet
     const u64 n = 1ULL << pf.logn;
     if (check_options(n, o)) return "UnacceptableProofOptions";
+    const int de = (int)o.ext;  // E = base field (1) or its quadratic extension (2)
     const u64 beta = o.beta, N = n * beta, depthN = pf.logn + ilog2(beta);
     const unsigned nl = num_fri_layers(N, o);
     if (pf.com.size() != 3 + nl || pf.fri_vals.size() != nl || pf.partitions != 0 || pf.num_unique == 0 ||
-        pf.ood.n != 14 * 8)
+        pf.ood.n != 14 * 8 * (size_t)de)
         return "ProofDeserializationError(\"inconsistent proof structure\")";
     const u64 nu = pf.num_unique;
-    if (pf.trace_rows.n != nu * 7 * 8 || pf.constraint_rows.n != nu * 8)
+    if (pf.trace_rows.n != nu * 7 * 8 || pf.constraint_rows.n != nu * 8 * de)
         return "ProofDeserializationError(\"query count\")";
+    auto draw = [&](Coin& coin, E2& out) {
+        u64 v[2] = {0, 0};
+        if (!coin.draw_e(v, de)) return false;
+        out = E2{v[0], v[1]};
+        return true;
+    };
 
     // ---- transcript
     u64 seed[20];
@@ -245,50 +255,57 @@ static std::string verify_proof(const uint8_t* bytes, size_t len, const AirConst
     Coin coin;
     coin.init(seed, 20);
     coin.reseed(pf.com[0]);
-    u64 alpha[7], bc[8];
+    E2 alpha[7], bc[8];
     for (auto& x : alpha)
-        if (!coin.draw(x)) return "RandomCoinError";
+        if (!draw(coin, x)) return "RandomCoinError";
     for (auto& x : bc)
-        if (!coin.draw(x)) return "RandomCoinError";
+        if (!draw(coin, x)) return "RandomCoinError";
     coin.reseed(pf.com[1]);
-    u64 z;
-    if (!coin.draw(z)) return "RandomCoinError";
-    const u64 g = gl_root((unsigned)pf.logn), zg = gl_mul(z, g), g_last = gl_pow(g, n - 1);
-    u64 ood[14];
-    for (int k = 0; k < 14; k++) ood[k] = pf.ood.elem(k);
+    E2 z;
+    if (!draw(coin, z)) return "RandomCoinError";
+    const u64 g = gl_root((unsigned)pf.logn), g_last = gl_pow(g, n - 1);
+    const E2 zg = e2_mulb(z, g);
+    E2 ood[14];
+    for (int k = 0; k < 14; k++) ood[k] = elem_e(pf.ood, k, de);
+    const E2 hz = elem_e(pf.hz, 0, de);
 
     // ---- OOD consistency: H(z) == sum alpha_i r_i(z) Z_t(z)^-1 + boundary terms
     {
-        u64 cur[7], nxt[7], rr[7];
+        E2 cur[7], nxt[7], rr[7];
         for (int c = 0; c < 7; c++) {
             cur[c] = ood[2 * c];
             nxt[c] = ood[2 * c + 1];
         }
         air_transition(air, cur, nxt, rr);
-        u64 t = 0;
-        for (int c = 0; c < 7; c++) t = gl_add(t, gl_mul(alpha[c], rr[c]));
-        const u64 zn1 = gl_sub(gl_pow(z, n), 1);
-        if (zn1 == 0 || z == 1 || z == g_last) return "InconsistentOodConstraintEvaluations";
-        u64 ev = gl_mul(gl_mul(t, gl_sub(z, g_last)), gl_inv(zn1));
+        E2 t{0, 0};
+        for (int c = 0; c < 7; c++) t = e2_add(t, e2_mul(alpha[c], rr[c]));
+        const E2 zn1 = e2_sub(e2_pow(z, n), e2(1)), z1 = e2_sub(z, e2(1)), zl = e2_sub(z, e2(g_last));
+        if (e2_eq(zn1, e2(0)) || e2_eq(z1, e2(0)) || e2_eq(zl, e2(0))) return "InconsistentOodConstraintEvaluations";
+        E2 ev = e2_mul(e2_mul(t, zl), e2_inv(zn1));
         const u64 v0[7] = {air.pub[0], air.pub[1], air.pub[2], air.pub[3], 0, air.nullifier, air.commitment};
-        u64 b0 = 0;
-        for (int c = 0; c < 7; c++) b0 = gl_add(b0, gl_mul(bc[c], gl_sub(cur[c], v0[c])));
-        const u64 b1 = gl_mul(bc[7], gl_sub(cur[4], 3));
-        ev = gl_add(ev, gl_mul(b0, gl_inv(gl_sub(z, 1))));
-        ev = gl_add(ev, gl_mul(b1, gl_inv(gl_sub(z, g_last))));
-        if (ev != pf.hz) return "InconsistentOodConstraintEvaluations";
+        E2 b0{0, 0};
+        for (int c = 0; c < 7; c++) b0 = e2_add(b0, e2_mul(bc[c], e2_sub(cur[c], e2(v0[c]))));
+        const E2 b1 = e2_mul(bc[7], e2_sub(cur[4], e2(3)));
+        ev = e2_add(ev, e2_mul(b0, e2_inv(z1)));
+        ev = e2_add(ev, e2_mul(b1, e2_inv(zl)));
+        if (!e2_eq(ev, hz)) return "InconsistentOodConstraintEvaluations";
     }
-    coin.reseed(hash_elements(ood, 14));
-    coin.reseed(hash_elements(&pf.hz, 1));
-    u64 dc[7], gam;
+    {
+        std::vector<u64> raw(15 * de);
+        memcpy(raw.data(), pf.ood.p, 14 * 8 * de);
+        memcpy(raw.data() + 14 * de, pf.hz.p, 8 * de);
+        coin.reseed(hash_elements(raw.data(), 14 * de));
+        coin.reseed(hash_elements(raw.data() + 14 * de, de));
+    }
+    E2 dc[7], gam;
     for (auto& x : dc)
-        if (!coin.draw(x)) return "RandomCoinError";
-    if (!coin.draw(gam)) return "RandomCoinError";
-    std::vector<u64> falpha(nl);
+        if (!draw(coin, x)) return "RandomCoinError";
+    if (!draw(coin, gam)) return "RandomCoinError";
+    std::vector<E2> falpha(nl);
     for (unsigned l = 0; l <= nl; l++) {
         coin.reseed(pf.com[2 + l]);
-        u64 a;
-        if (!coin.draw(a)) return "RandomCoinError";
+        E2 a;
+        if (!draw(coin, a)) return "RandomCoinError";
         if (l < nl) falpha[l] = a;
     }
     // ---- proof of work + query positions
@@ -312,24 +329,24 @@ static std::string verify_proof(const uint8_t* bytes, size_t len, const AirConst
     for (u64 i = 0; i < nu; i++) leaves[i] = leaf_hash(pf.trace_rows.p + i * 56, 56);
     if (!batch_root(pos, leaves, pf.trace_paths, N, root) || !same(root, pf.com[0]))
         return "TraceQueryDoesNotMatchCommitment";
-    for (u64 i = 0; i < nu; i++) leaves[i] = leaf_hash(pf.constraint_rows.p + i * 8, 8);
+    for (u64 i = 0; i < nu; i++) leaves[i] = leaf_hash(pf.constraint_rows.p + i * 8 * de, 8 * de);
     if (!batch_root(pos, leaves, pf.constraint_paths, N, root) || !same(root, pf.com[1]))
         return "ConstraintQueryDoesNotMatchCommitment";
 
     // ---- DEEP composition at the query points
-    std::vector<u64> ev(nu);
+    std::vector<E2> ev(nu);
     const u64 wN = gl_root((unsigned)depthN);
     for (u64 i = 0; i < nu; i++) {
-        const u64 x = gl_mul(GEN, gl_pow(wN, pos[i]));
-        u64 s1 = 0, s2 = 0;
+        const E2 x = e2(gl_mul(GEN, gl_pow(wN, pos[i])));
+        E2 s1{0, 0}, s2{0, 0};
         for (int c = 0; c < 7; c++) {
-            const u64 tx = pf.trace_rows.elem(i * 7 + c);
-            s1 = gl_add(s1, gl_mul(dc[c], gl_sub(tx, ood[2 * c])));
-            s2 = gl_add(s2, gl_mul(dc[c], gl_sub(tx, ood[2 * c + 1])));
+            const E2 tx = e2(pf.trace_rows.elem(i * 7 + c));
+            s1 = e2_add(s1, e2_mul(dc[c], e2_sub(tx, ood[2 * c])));
+            s2 = e2_add(s2, e2_mul(dc[c], e2_sub(tx, ood[2 * c + 1])));
         }
-        const u64 izx = gl_inv(gl_sub(x, z)), izgx = gl_inv(gl_sub(x, zg));
-        u64 d = gl_add(gl_mul(s1, izx), gl_mul(s2, izgx));
-        d = gl_add(d, gl_mul(gl_mul(gam, gl_sub(pf.constraint_rows.elem(i), pf.hz)), izx));
+        const E2 izx = e2_inv(e2_sub(x, z)), izgx = e2_inv(e2_sub(x, zg));
+        E2 d = e2_add(e2_mul(s1, izx), e2_mul(s2, izgx));
+        d = e2_add(d, e2_mul(e2_mul(gam, e2_sub(elem_e(pf.constraint_rows, i, de), hz)), izx));
         ev[i] = d;
     }
 
@@ -340,38 +357,39 @@ static std::string verify_proof(const uint8_t* bytes, size_t len, const AirConst
         const u64 rows = D / 8;
         std::vector<u64> fp = fold_positions(cur, rows);
         const Span& vals = pf.fri_vals[l];
-        if (vals.n != fp.size() * 64) return "FriVerificationFailed(InvalidLayerCommitment)";
+        if (vals.n != fp.size() * 64 * de) return "FriVerificationFailed(InvalidLayerCommitment)";
         std::vector<Digest> lv(fp.size());
-        for (size_t i = 0; i < fp.size(); i++) lv[i] = leaf_hash(vals.p + i * 64, 64);
+        for (size_t i = 0; i < fp.size(); i++) lv[i] = leaf_hash(vals.p + i * 64 * de, 64 * de);
         if (!batch_root(fp, lv, pf.fri_paths[l], rows, root) || !same(root, pf.com[2 + l]))
             return "FriVerificationFailed(LayerCommitmentMismatch)";
         for (size_t i = 0; i < cur.size(); i++) {
             const u64 ri = cur[i] & (rows - 1), k = cur[i] / rows;
             const size_t at = std::find(fp.begin(), fp.end(), ri) - fp.begin();
-            if (vals.elem(at * 8 + k) != ev[i]) return "FriVerificationFailed(InvalidLayerFolding)";
+            if (!e2_eq(elem_e(vals, at * 8 + k, de), ev[i])) return "FriVerificationFailed(InvalidLayerFolding)";
         }
         const u64 wD = gl_root(ilog2(D));
-        std::vector<u64> nev(fp.size());
+        std::vector<E2> nev(fp.size());
         for (size_t i = 0; i < fp.size(); i++) {
-            u64 v[8];
-            for (int k = 0; k < 8; k++) v[k] = vals.elem(i * 8 + k);
+            E2 v[8];
+            for (int k = 0; k < 8; k++) v[k] = elem_e(vals, i * 8 + k, de);
             nev[i] = fold_row(v, gl_mul(GEN, gl_pow(wD, fp[i])), falpha[l]);
         }
         cur.swap(fp);
         ev.swap(nev);
         D = rows;
     }
-    const u64 rl = pf.fri_rem.n / 8;
+    const u64 rl = pf.fri_rem.n / (8 * de);
     if (rl == 0 || rl != D / beta) return "FriVerificationFailed(InvalidRemainderFolding)";
-    std::vector<u64> rem(rl);
-    for (u64 i = 0; i < rl; i++) rem[i] = pf.fri_rem.elem(i);
-    if (!same(hash_elements(rem.data(), rl), pf.com[2 + nl])) return "FriVerificationFailed(RemainderCommitmentMismatch)";
+    std::vector<u64> raw(rl * de);
+    memcpy(raw.data(), pf.fri_rem.p, rl * 8 * de);
+    if (!same(hash_elements(raw.data(), rl * de), pf.com[2 + nl]))
+        return "FriVerificationFailed(RemainderCommitmentMismatch)";
     const u64 wD = gl_root(ilog2(D));
     for (size_t i = 0; i < cur.size(); i++) {
-        const u64 x = gl_mul(GEN, gl_pow(wD, cur[i]));
-        u64 r = 0;
-        for (u64 k = rl; k-- > 0;) r = gl_add(gl_mul(r, x), rem[k]);
-        if (r != ev[i]) return "FriVerificationFailed(InvalidRemainderFolding)";
+        const E2 x = e2(gl_mul(GEN, gl_pow(wD, cur[i])));
+        E2 r{0, 0};
+        for (u64 k = rl; k-- > 0;) r = e2_add(e2_mul(r, x), elem_e(pf.fri_rem, k, de));
+        if (!e2_eq(r, ev[i])) return "FriVerificationFailed(InvalidRemainderFolding)";
     }
     return "";
 }
@@ -418,8 +436,9 @@ int xfg_proof_parse(const uint8_t* proof, size_t len, xfg_proof_info* info, char
     info->pow_nonce = pf.nonce;
     info->size = pf.size;
     for (size_t i = 0; i < 2 && i < pf.com.size(); i++) memcpy(i ? info->constraint_root : info->trace_root, pf.com[i].w, 32);
-    for (int k = 0; k < 14; k++) info->ood_trace[k] = pf.ood.elem(k);
-    info->ood_composition = pf.hz;
+    const int de = pf.o.ext == 2 ? 2 : 1;  // with an extension: first coordinates
+    for (int k = 0; k < 14; k++) info->ood_trace[k] = pf.ood.elem((size_t)k * de);
+    info->ood_composition = pf.hz.elem(0);
     return XFG_OK;
 }
 
