@@ -27,14 +27,20 @@ DEF(k_mullo, "v_mul_lo_u32 %0, %0, %1")
 DEF(k_mulhi, "v_mul_hi_u32 %0, %0, %1")
 DEF(k_addco, "v_add_co_u32 %0, vcc, %0, %1")
 DEF(k_lshl_or, "v_lshl_or_b32 %0, %0, 7, %1")
+DEF(k_sdwa_xor, "v_xor_b32_sdwa %0, %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0")
+DEF(k_sdwa_add, "v_add_u32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD")
+DEF(k_cndmask, "v_cndmask_b32_e32 %0, %0, %1, vcc")
+DEF(k_lshrrev, "v_lshrrev_b32_e32 %0, 7, %0")
 int main() {
     unsigned* d;
-    const int blocks = 256 * 8, threads = 256, iters = 256;
+    const int blocks = 256 * 8, threads = 256, iters = 2048;
     hipMalloc(&d, (size_t)blocks * threads * 4);
     struct { const char* n; void (*f)(unsigned*, int); } ks[] = {
         {"v_add_u32", k_add}, {"v_xor_b32", k_xor}, {"v_add3_u32", k_add3}, {"v_alignbit_b32", k_alignbit},
         {"v_xad_u32", k_xad}, {"v_bitop3_b32", k_bitop3}, {"v_perm_b32", k_perm}, {"v_mad_u32_u24", k_mad32},
-        {"v_mul_lo_u32", k_mullo}, {"v_mul_hi_u32", k_mulhi}, {"v_add_co_u32", k_addco}, {"v_lshl_or_b32", k_lshl_or}};
+        {"v_mul_lo_u32", k_mullo}, {"v_mul_hi_u32", k_mulhi}, {"v_add_co_u32", k_addco}, {"v_lshl_or_b32", k_lshl_or},
+        {"v_xor_b32_sdwa", k_sdwa_xor}, {"v_add_u32_sdwa", k_sdwa_add}, {"v_cndmask_b32", k_cndmask},
+        {"v_lshrrev_b32", k_lshrrev}};
     for (auto& k : ks) {
         hipEvent_t a, b;
         hipEventCreate(&a);
