@@ -153,6 +153,12 @@ int xfg_verify(const uint8_t* proof, size_t len, const xfg_air_consts* air, cons
 int xfg_verify_batch(uint32_t count, const uint8_t* const* proofs, const size_t* lens, const xfg_air_consts* airs,
                      const xfg_options* acceptable, int* results, uint32_t threads);
 
+/* batched verification on the context's GPU: the host replays each transcript (threads), the device
+ * recomputes every Merkle opening (leaf hashes, then one launch per tree level for all proofs) and
+ * runs the per-query DEEP / FRI / remainder checks. results[i] as xfg_verify. */
+int xfg_verify_batch_gpu(xfg_ctx* ctx, uint32_t count, const uint8_t* const* proofs, const size_t* lens,
+                         const xfg_air_consts* airs, const xfg_options* acceptable, int* results);
+
 /* ---- instrumentation (benchmarks / parity tests) ---- */
 /* host BLAKE3 of the library (any length), for self-tests */
 int xfg_selftest_blake3(const uint8_t* in, size_t len, uint8_t out[32]);

@@ -305,6 +305,35 @@ def test_config5_quadratic_2p20_blowup16(prover):
     assert prover.prove_burn_mint(**kw, trace_length=1 << 20).to_bytes() == p1
 
 
+@pytest.mark.parametrize("ext,n,blowup", [(1, 1024, 8), (2, 512, 16), (1, 1 << 16, 8)])
+def test_gpu_batch_verify_matches_host_verifier(prover, ext, n, blowup):
+    """xfg_verify_batch_gpu: same verdicts as the host verifier on GPU-made proofs, valid and
+    tampered (every section), wrong statements and wrong options"""
+    import xfgstark
+    o = xfgstark.ProofOptions.reference()
+    o.field_extension, o.blowup_factor = ext, blowup
+    prover._options = o
+    kws = [synthetic.burn_inputs(2100 + i) for i in range(6)]
+    proofs = [p.to_bytes() for p in prover.prove_batch(kws, trace_length=n)]
+    airs = [xfgstark.air_consts(**kw) for kw in kws]
+    items = []
+    for p, a in zip(proofs, airs):
+        items.append((p, a))
+        for frac in (0.05, 0.2, 0.35, 0.5, 0.7, 0.9, 0.995):  # flips across the proof sections
+            b = bytearray(p)
+            b[int(len(b) * frac)] ^= 0x10
+            items.append((bytes(b), a))
+        items.append((p, (a[0], a[1] ^ 1, a[2])))
+    v = xfgstark.XfgBurnMintVerifier(proof_options=o)
+    host = v.batch_verify(items)
+    dev = v.batch_verify(items, gpu=prover)
+    assert dev == host
+    assert sum(host) == len(proofs)  # exactly the untampered proofs with their own statement
+    other = xfgstark.ProofOptions.reference()
+    other.num_queries = 41
+    assert not any(xfgstark.XfgBurnMintVerifier(proof_options=other).batch_verify(items[:3], gpu=prover))
+
+
 def test_rejects_options_the_reference_rejects(prover):
     import xfgstark
     kw = synthetic.burn_inputs(3)

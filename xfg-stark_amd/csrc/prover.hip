@@ -24,6 +24,7 @@
 #include "../../include/xfg_stark.h"
 #include "host_common.hpp"
 #include "kernels.hpp"
+#include "verifier.hpp"
 
 namespace xfg {
 
@@ -305,6 +306,17 @@ struct xfg_ctx {
     uint64_t next_ticket = 1;
     std::map<uint64_t, std::unique_ptr<xfg::Batch>> pending;
     int last_lane = 0;
+    // batched GPU verification workspace (xfg_verify_batch_gpu)
+    struct {
+        xfg::DBuf<uint8_t> blob;
+        xfg::DBuf<xfg::VGather> g;
+        xfg::DBuf<xfg::VLeaf> lv;
+        xfg::DBuf<uint32_t> rounds, flags;
+        xfg::DBuf<xfg::VFieldProof> fp;
+        xfg::DBuf<xfg::VFieldQuery> fq;
+        xfg::DBuf<xfg::Digest> dig, rootdig;
+        xfg::DBuf<uint64_t> rootidx;
+    } vb;
 };
 
 namespace xfg {
@@ -1536,6 +1548,115 @@ int xfg_debug_ood_deep(xfg_ctx* c, uint32_t count, uint64_t n, const uint64_t* c
         launch_deep(L->coef.p, L->hcoef.p, L->dp.p, L->partial.p, L->carry.p, L->deep.p, logn, (int)B, 1, s);
         HIPCHK(hipMemcpyAsync(deep_out, L->deep.p, B * n * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
+        return XFG_OK;
+    });
+}
+
+int xfg_verify_batch_gpu(xfg_ctx* c, uint32_t count, const uint8_t* const* proofs, const size_t* lens,
+                         const xfg_air_consts* airs, const xfg_options* acceptable, int* results) {
+    if (!c || !proofs || !lens || !airs || !acceptable || !results) return XFG_INVALID_ARGUMENT;
+    c->err.clear();
+    if (busy(c)) {
+        c->err = "batches pending: call xfg_batch_wait first";
+        return XFG_INVALID_ARGUMENT;
+    }
+    return guarded(c, [&]() -> int {
+        HIPCHK(hipSetDevice(c->device));
+        const Opts acc = to_opts(acceptable);
+        std::vector<VState> st(count);
+        std::vector<std::string> err(count);
+        const unsigned nt = std::max(1u, std::min<unsigned>(std::thread::hardware_concurrency(), 16));
+        auto parallel = [&](const std::function<void(uint32_t)>& f) {
+            std::vector<std::thread> th;
+            for (unsigned t = 0; t < nt; t++)
+                th.emplace_back([&, t] {
+                    for (uint32_t i = t; i < count; i += nt) f(i);
+                });
+            for (auto& x : th) x.join();
+        };
+        // 1. transcripts (host threads)
+        parallel([&](uint32_t i) {
+            if (!proofs[i]) {
+                err[i] = "null proof";
+                return;
+            }
+            try {
+                err[i] = verify_transcript(proofs[i], lens[i], air_of(&airs[i]), acc, st[i]);
+            } catch (const std::exception& e) {
+                err[i] = std::string("ProofDeserializationError(\"") + e.what() + "\")";
+            }
+        });
+        // 2. plan: blob of all proofs, Merkle tasks, field queries
+        VerifyPlan plan;
+        std::vector<int> planned(count, -1);
+        size_t total = 0;
+        for (uint32_t i = 0; i < count; i++) total += (proofs[i] ? lens[i] : 0);
+        plan.blob.reserve(total);
+        for (uint32_t i = 0; i < count; i++) {
+            if (!err[i].empty()) continue;
+            const size_t off = plan.blob.size();
+            plan.blob.insert(plan.blob.end(), proofs[i], proofs[i] + lens[i]);
+            std::string e;
+            if (plan_proof(st[i], off, plan, e)) planned[i] = (int)plan.roots.size() - 1;
+            else err[i] = e;
+        }
+        // 3. device work
+        std::vector<u64> ridx;
+        for (auto& rs : plan.roots)
+            for (int64_t r : rs) ridx.push_back(r >= 0 ? (u64)r : 0);
+        std::vector<Digest> rootd(ridx.size());
+        std::vector<uint32_t> flags(plan.fproofs.size(), 0);
+        if (!plan.roots.empty()) {
+            auto& V = c->vb;
+            hipStream_t s = lane0(c)->stream;
+            std::vector<uint32_t> rounds;
+            std::vector<u64> roff{0};
+            for (auto& r : plan.rounds) {
+                rounds.insert(rounds.end(), r.begin(), r.end());
+                roff.push_back(rounds.size());
+            }
+            V.blob.ensure(plan.blob.size());
+            V.g.ensure(std::max<size_t>(1, plan.gathers.size()));
+            V.lv.ensure(std::max<size_t>(1, plan.leaves.size()));
+            V.rounds.ensure(std::max<size_t>(1, rounds.size()));
+            V.fp.ensure(plan.fproofs.size());
+            V.fq.ensure(std::max<size_t>(1, plan.fqueries.size()));
+            V.dig.ensure(std::max<uint32_t>(1, plan.nslots));
+            V.flags.ensure(plan.fproofs.size());
+            V.rootidx.ensure(ridx.size());
+            V.rootdig.ensure(ridx.size());
+            HIPCHK(hipMemcpyAsync(V.blob.p, plan.blob.data(), plan.blob.size(), hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(V.g.p, plan.gathers.data(), plan.gathers.size() * sizeof(VGather), hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(V.lv.p, plan.leaves.data(), plan.leaves.size() * sizeof(VLeaf), hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(V.rounds.p, rounds.data(), rounds.size() * 4, hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(V.fp.p, plan.fproofs.data(), plan.fproofs.size() * sizeof(VFieldProof),
+                                  hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(V.fq.p, plan.fqueries.data(), plan.fqueries.size() * sizeof(VFieldQuery),
+                                  hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(V.rootidx.p, ridx.data(), ridx.size() * 8, hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemsetAsync(V.flags.p, 0, plan.fproofs.size() * 4, s));
+            launch_verify(V.blob.p, V.g.p, plan.gathers.size(), V.lv.p, plan.leaves.size(), V.rounds.p, roff.data(),
+                          (int)plan.rounds.size(), V.fp.p, V.fq.p, plan.fqueries.size(), V.dig.p, V.flags.p, s);
+            launch_gather_digest(V.dig.p, V.rootidx.p, V.rootdig.p, ridx.size(), s);
+            HIPCHK(hipMemcpyAsync(rootd.data(), V.rootdig.p, ridx.size() * sizeof(Digest), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipMemcpyAsync(flags.data(), V.flags.p, flags.size() * 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+        }
+        // 4. verdicts in the host verifier's check order
+        std::vector<size_t> rbase(plan.roots.size() + 1, 0);
+        for (size_t k = 0; k < plan.roots.size(); k++) rbase[k + 1] = rbase[k] + plan.roots[k].size();
+        parallel([&](uint32_t i) {
+            if (planned[i] >= 0) {
+                const int k = planned[i];
+                std::vector<Digest> rd(plan.roots[k].size());
+                for (size_t t = 0; t < rd.size(); t++) {
+                    if (plan.roots[k][t] >= 0) rd[t] = rootd[rbase[k] + t];
+                    else memset(rd[t].w, 0xFF, 32);
+                }
+                err[i] = finish_proof(st[i], rd, flags[plan.fidx[k]]);
+            }
+            results[i] = proofs[i] ? (err[i].empty() ? XFG_OK : XFG_VERIFY_FAILED) : XFG_INVALID_ARGUMENT;
+        });
         return XFG_OK;
     });
 }

@@ -13,8 +13,7 @@
 #include <unordered_map>
 #include <vector>
 
-#include "host_common.hpp"
-#include "kernels.hpp"
+#include "verifier.hpp"
 
 namespace xfg {
 
@@ -40,47 +39,19 @@ struct Reader {
         return v;
     }
 };
-struct Span {
-    const uint8_t* p = nullptr;
-    size_t n = 0;
-    u64 elem(size_t i) const {
-        u64 v;
-        memcpy(&v, p + 8 * i, 8);
-        return v;
-    }
-};
-// BatchMerkleProof::serialize_nodes: u8 vector count, then per vector u8 count + digests
-struct Paths {
-    std::vector<std::vector<Digest>> vecs;
-};
-
-// StarkProof fields in wire order (DESIGN.md "Proof format")
-struct ParsedProof {
-    u64 width = 0, aux = 0, logn = 0;
-    Opts o{};
-    u64 num_unique = 0;
-    std::vector<Digest> com;  // trace root, constraint root, FRI layer roots, remainder commitment
-    Span trace_rows, constraint_rows, ood, fri_rem;
-    Paths trace_paths, constraint_paths;
-    Span hz;
-    std::vector<Span> fri_vals;
-    std::vector<Paths> fri_paths;
-    u64 partitions = 0, nonce = 0;
-    size_t size = 0;
-};
-
 static bool read_paths(Reader& r, size_t len, Paths& out) {
     const uint8_t* q = r.take(len);
     if (!q) return false;
     Reader s{q, len};
     const u64 m = s.u(1);
-    out.vecs.resize(m);
+    out.ptr.resize(m);
+    out.cnt.resize(m);
     for (u64 i = 0; i < m; i++) {
         const u64 c = s.u(1);
         const uint8_t* d = s.take(c * 32);
         if (!d) return false;
-        out.vecs[i].resize(c);
-        memcpy(out.vecs[i].data(), d, c * 32);
+        out.ptr[i] = d;
+        out.cnt[i] = (uint32_t)c;
     }
     return !s.bad && s.off == len;
 }
@@ -91,8 +62,9 @@ static bool read_span(Reader& r, int len_bytes, Span& s) {
 }
 
 // returns "" on success, else the ProofDeserializationError text
-static std::string parse_proof(const uint8_t* bytes, size_t len, ParsedProof& pf) {
+std::string parse_proof(const uint8_t* bytes, size_t len, ParsedProof& pf) {
     Reader r{bytes, len};
+    pf.base = bytes;
     pf.width = r.u(1);
     pf.aux = r.u(1);
     pf.logn = r.u(1);
@@ -149,36 +121,55 @@ static std::string parse_proof(const uint8_t* bytes, size_t len, ParsedProof& pf
 
 // ------------------------------------------------------------------ batch Merkle root
 // BatchMerkleProof::get_root: the node vectors must hold exactly the siblings the opening plan of
-// `idx` asks for; every node on the way to the root is then recomputed.
-static bool batch_root(const std::vector<u64>& idx, const std::vector<Digest>& leaf, const Paths& paths, u64 L,
-                       Digest& root) {
+// `idx` asks for; every node on the way to the root is then recomputed, level by level.
+bool merkle_symbolic(const std::vector<u64>& idx, const Paths& paths, u64 L, MerkleSym& out) {
     BatchOpening plan;
     plan_batch_opening(idx, L, plan);
-    if (plan.size() != paths.vecs.size()) return false;
-    std::unordered_map<u64, Digest> known;
-    known.reserve(4 * (idx.size() + 1) * (ilog2(L) + 1));
-    for (size_t i = 0; i < idx.size(); i++) known[L + idx[i]] = leaf[i];
+    out.given.clear();
+    out.levels.clear();
+    if (plan.size() != paths.ptr.size()) return false;
+    std::vector<u64> known;  // heap indices available so far
+    for (u64 i : idx) known.push_back(L + i);
     for (size_t i = 0; i < plan.size(); i++) {
-        if (paths.vecs[i].size() != plan.len[i]) return false;
-        for (unsigned k = 0; k < plan.len[i]; k++) known[plan.row(i)[k]] = paths.vecs[i][k];
+        if (paths.cnt[i] != plan.len[i]) return false;
+        for (unsigned k = 0; k < plan.len[i]; k++) {
+            out.given.push_back({plan.row(i)[k], paths.ptr[i] + 32 * k});
+            known.push_back(plan.row(i)[k]);
+        }
     }
+    std::sort(known.begin(), known.end());
+    known.erase(std::unique(known.begin(), known.end()), known.end());
+    auto has = [&](u64 h) { return std::binary_search(known.begin(), known.end(), h); };
     std::vector<u64> level;
     for (u64 i : idx) level.push_back(L + i);
     std::sort(level.begin(), level.end());
     level.erase(std::unique(level.begin(), level.end()), level.end());
     while (!(level.size() == 1 && level[0] == 1)) {
-        std::vector<u64> up;
+        std::vector<u64> up, trip;
         for (u64 x : level) {
             const u64 p = x >> 1;
             if (!up.empty() && up.back() == p) continue;
-            auto a = known.find(2 * p), b = known.find(2 * p + 1);
-            if (a == known.end() || b == known.end()) return false;
-            known[p] = b3_merge(a->second, b->second);
+            if (!has(2 * p) || !has(2 * p + 1)) return false;
+            trip.insert(trip.end(), {p, 2 * p, 2 * p + 1});
             up.push_back(p);
         }
+        for (u64 p : up) known.insert(std::upper_bound(known.begin(), known.end(), p), p);
+        out.levels.push_back(std::move(trip));
         level.swap(up);
     }
-    root = known[1];
+    return true;
+}
+static bool batch_root(const std::vector<u64>& idx, const std::vector<Digest>& leaf, const Paths& paths, u64 L,
+                       Digest& root) {
+    MerkleSym sym;
+    if (!merkle_symbolic(idx, paths, L, sym)) return false;
+    std::unordered_map<u64, Digest> val;
+    val.reserve(2 * (sym.given.size() + idx.size()) + 64);
+    for (size_t i = 0; i < idx.size(); i++) val[L + idx[i]] = leaf[i];
+    for (auto& g : sym.given) memcpy(val[g.first].w, g.second, 32);
+    for (auto& lv : sym.levels)
+        for (size_t t = 0; t < lv.size(); t += 3) val[lv[t]] = b3_merge(val[lv[t + 1]], val[lv[t + 2]]);
+    root = val[1];
     return true;
 }
 static bool same(const Digest& a, const Digest& b) { return !memcmp(a.w, b.w, 32); }
@@ -223,8 +214,9 @@ static E2 fold_row(const E2 v[8], u64 x, E2 alpha) {
 static E2 elem_e(const Span& s, size_t i, int de) { return de == 2 ? E2{s.elem(2 * i), s.elem(2 * i + 1)} : e2(s.elem(i)); }
 
 // returns "" when the proof verifies, else the VerifierError (Debug form)
-static std::string verify_proof(const uint8_t* bytes, size_t len, const AirConst& air, const Opts& acceptable) {
-    ParsedProof pf;
+std::string verify_transcript(const uint8_t* bytes, size_t len, const AirConst& air, const Opts& acceptable,
+                              VState& st) {
+    ParsedProof& pf = st.pf;
     std::string e = parse_proof(bytes, len, pf);
     if (!e.empty()) return e;
     if (pf.width != 7 || pf.aux != 0) return "InconsistentTraceWidth";
@@ -233,7 +225,7 @@ static std::string verify_proof(const uint8_t* bytes, size_t len, const AirConst
     const u64 n = 1ULL << pf.logn;
     if (check_options(n, o)) return "UnacceptableProofOptions";
     const int de = (int)o.ext;  // E = base field (1) or its quadratic extension (2)
-    const u64 beta = o.beta, N = n * beta, depthN = pf.logn + ilog2(beta);
+    const u64 beta = o.beta, N = n * beta;
     const unsigned nl = num_fri_layers(N, o);
     if (pf.com.size() != 3 + nl || pf.fri_vals.size() != nl || pf.partitions != 0 || pf.num_unique == 0 ||
         pf.ood.n != 14 * 8 * (size_t)de)
@@ -323,6 +315,32 @@ static std::string verify_proof(const uint8_t* bytes, size_t len, const AirConst
     pos.erase(std::unique(pos.begin(), pos.end()), pos.end());
     if (pos.size() != nu) return "ProofDeserializationError(\"number of unique queries\")";
 
+    st.de = de;
+    st.n = n;
+    st.N = N;
+    st.beta = beta;
+    st.nl = nl;
+    st.pos = std::move(pos);
+    st.z = z;
+    st.zg = zg;
+    st.hz = hz;
+    for (int k = 0; k < 14; k++) st.ood[k] = ood[k];
+    for (int k = 0; k < 7; k++) st.dc[k] = dc[k];
+    st.gam = gam;
+    st.falpha = std::move(falpha);
+    return "";
+}
+
+std::string verify_queries_host(const VState& st) {
+    const ParsedProof& pf = st.pf;
+    const int de = st.de;
+    const u64 N = st.N, beta = st.beta, nu = pf.num_unique, depthN = ilog2(N);
+    const unsigned nl = st.nl;
+    const std::vector<u64>& pos = st.pos;
+    const E2 z = st.z, zg = st.zg, hz = st.hz, gam = st.gam;
+    const E2* ood = st.ood;
+    const E2* dc = st.dc;
+    const std::vector<E2>& falpha = st.falpha;
     // ---- trace / constraint openings
     std::vector<Digest> leaves(nu);
     Digest root;
@@ -394,7 +412,146 @@ static std::string verify_proof(const uint8_t* bytes, size_t len, const AirConst
     return "";
 }
 
-static AirConst air_of(const xfg_air_consts* a) {
+static std::string verify_proof(const uint8_t* bytes, size_t len, const AirConst& air, const Opts& acceptable) {
+    VState st;
+    std::string e = verify_transcript(bytes, len, air, acceptable, st);
+    return e.empty() ? verify_queries_host(st) : e;
+}
+
+// ------------------------------------------------------------------ batched GPU verification plan
+bool plan_proof(const VState& st, size_t blob_off, VerifyPlan& plan, std::string& err) {
+    const ParsedProof& pf = st.pf;
+    const int de = st.de;
+    const u64 N = st.N, nu = pf.num_unique;
+    const unsigned nl = st.nl;
+    if (nl > (unsigned)VMAXL) {
+        err = "ProofDeserializationError(\"too many FRI layers\")";
+        return false;
+    }
+    auto off = [&](const uint8_t* p) { return (u64)blob_off + (u64)(p - pf.base); };
+    // FRI position lists and the structural checks of the host verifier
+    std::vector<std::vector<u64>> fps(nl);
+    {
+        std::vector<u64> cur = st.pos;
+        u64 D = N;
+        for (unsigned l = 0; l < nl; l++) {
+            const u64 rows = D / 8;
+            fps[l] = fold_positions(cur, rows);
+            if (pf.fri_vals[l].n != fps[l].size() * 64 * de) {
+                err = "FriVerificationFailed(InvalidLayerCommitment)";
+                return false;
+            }
+            cur = fps[l];
+            D = rows;
+        }
+        const u64 rl = pf.fri_rem.n / (8 * de);
+        if (rl == 0 || rl != D / st.beta) {
+            err = "FriVerificationFailed(InvalidRemainderFolding)";
+            return false;
+        }
+    }
+    // Merkle trees: leaves, given nodes, merges by level -> digest slots
+    std::vector<int64_t> roots;
+    auto add_tree = [&](const std::vector<u64>& idx, const Paths& paths, u64 L, const uint8_t* leaf0, size_t stride,
+                        uint32_t words) -> int64_t {
+        MerkleSym sym;
+        if (!merkle_symbolic(idx, paths, L, sym)) return -1;
+        std::unordered_map<u64, uint32_t> slot;
+        slot.reserve(2 * (idx.size() + sym.given.size()) + 64);
+        for (size_t i = 0; i < idx.size(); i++) {
+            const uint32_t sl = plan.nslots++;
+            slot[L + idx[i]] = sl;
+            plan.leaves.push_back(VLeaf{off(leaf0 + i * stride), words, sl});
+        }
+        for (auto& g : sym.given) {
+            const uint32_t sl = plan.nslots++;
+            slot[g.first] = sl;
+            plan.gathers.push_back(VGather{off(g.second), sl, 0});
+        }
+        if (plan.rounds.size() < sym.levels.size()) plan.rounds.resize(sym.levels.size());
+        for (size_t r = 0; r < sym.levels.size(); r++) {
+            const auto& lv = sym.levels[r];
+            for (size_t t = 0; t < lv.size(); t += 3) {
+                const uint32_t sl = plan.nslots++;
+                const uint32_t a = slot[lv[t + 1]], b = slot[lv[t + 2]];
+                slot[lv[t]] = sl;
+                plan.rounds[r].insert(plan.rounds[r].end(), {sl, a, b});
+            }
+        }
+        return slot[1];
+    };
+    roots.push_back(add_tree(st.pos, pf.trace_paths, N, pf.trace_rows.p, 56, 7));
+    roots.push_back(add_tree(st.pos, pf.constraint_paths, N, pf.constraint_rows.p, 8 * de, (uint32_t)de));
+    {
+        u64 D = N;
+        for (unsigned l = 0; l < nl; l++) {
+            const u64 rows = D / 8;
+            roots.push_back(add_tree(fps[l], pf.fri_paths[l], rows, pf.fri_vals[l].p, 64 * de, (uint32_t)(8 * de)));
+            D = rows;
+        }
+    }
+    plan.roots.push_back(roots);
+    // field checks
+    VFieldProof F{};
+    F.z = st.z;
+    F.zg = st.zg;
+    F.hz = st.hz;
+    F.gam = st.gam;
+    for (int k = 0; k < 7; k++) F.dc[k] = st.dc[k];
+    for (int k = 0; k < 14; k++) F.ood[k] = st.ood[k];
+    for (unsigned l = 0; l < nl; l++) F.falpha[l] = st.falpha[l];
+    F.rem_off = off(pf.fri_rem.p);
+    F.rem_len = (uint32_t)(pf.fri_rem.n / (8 * de));
+    F.nl = nl;
+    F.de = (uint32_t)de;
+    F.logN = ilog2(N);
+    const uint32_t fi = (uint32_t)plan.fproofs.size();
+    plan.fproofs.push_back(F);
+    plan.fidx.push_back((int)fi);
+    for (u64 i = 0; i < nu; i++) {
+        VFieldQuery Q{};
+        Q.proof = fi;
+        Q.pos = st.pos[i];
+        Q.trace_off = off(pf.trace_rows.p + i * 56);
+        Q.cons_off = off(pf.constraint_rows.p + i * 8 * de);
+        u64 p = st.pos[i], D = N;
+        for (unsigned l = 0; l < nl; l++) {
+            const u64 rows = D / 8, r = p & (rows - 1);
+            const size_t at = std::find(fps[l].begin(), fps[l].end(), r) - fps[l].begin();
+            Q.row_off[l] = off(pf.fri_vals[l].p + at * 64 * de);
+            p = r;
+            D = rows;
+        }
+        plan.fqueries.push_back(Q);
+    }
+    return true;
+}
+
+std::string finish_proof(const VState& st, const std::vector<Digest>& roots, uint32_t flags) {
+    const ParsedProof& pf = st.pf;
+    // roots[t] for the 2 + nl trees (an all-ones digest marks a structurally invalid opening)
+    auto bad_root = [&](size_t t) {
+        const Digest& d = roots[t];
+        bool invalid = true;
+        for (int w = 0; w < 8; w++) invalid = invalid && d.w[w] == 0xFFFFFFFFu;
+        return invalid || !same(d, pf.com[t]);
+    };
+    if (bad_root(0)) return "TraceQueryDoesNotMatchCommitment";
+    if (bad_root(1)) return "ConstraintQueryDoesNotMatchCommitment";
+    for (unsigned l = 0; l < st.nl; l++) {
+        if (bad_root(2 + l)) return "FriVerificationFailed(LayerCommitmentMismatch)";
+        if (flags & (1u << l)) return "FriVerificationFailed(InvalidLayerFolding)";
+    }
+    const u64 rl = pf.fri_rem.n / (8 * st.de);
+    std::vector<u64> raw(rl * st.de);
+    memcpy(raw.data(), pf.fri_rem.p, rl * 8 * st.de);
+    if (!same(hash_elements(raw.data(), rl * st.de), pf.com[2 + st.nl]))
+        return "FriVerificationFailed(RemainderCommitmentMismatch)";
+    if (flags & (1u << 31)) return "FriVerificationFailed(InvalidRemainderFolding)";
+    return "";
+}
+
+AirConst air_of(const xfg_air_consts* a) {
     AirConst c;
     memset(&c, 0, sizeof c);
     memcpy(c.pub, a->pub_inputs, sizeof a->pub_inputs);

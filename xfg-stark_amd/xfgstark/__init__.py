@@ -72,6 +72,8 @@ _lib.xfg_proof_parse.argtypes = [_u8p, C.c_size_t, C.POINTER(_ProofInfo), C.c_ch
 _lib.xfg_verify.argtypes = [_u8p, C.c_size_t, C.POINTER(_AirConsts), C.POINTER(_Options), C.c_char_p, C.c_size_t]
 _lib.xfg_verify_batch.argtypes = [C.c_uint32, C.POINTER(_u8p), C.POINTER(C.c_size_t), C.POINTER(_AirConsts),
                                   C.POINTER(_Options), C.POINTER(C.c_int), C.c_uint32]
+_lib.xfg_verify_batch_gpu.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(_u8p), C.POINTER(C.c_size_t),
+                                      C.POINTER(_AirConsts), C.POINTER(_Options), C.POINTER(C.c_int)]
 _lib.xfg_selftest_blake3.argtypes = [_u8p, C.c_size_t, _u8p]
 _lib.xfg_prepare.argtypes = [C.c_void_p, C.c_uint32, C.c_uint64, C.POINTER(_Options)]
 _lib.xfg_burn_air_consts.argtypes = [C.POINTER(_BurnInputs), C.POINTER(_AirConsts)]
@@ -246,8 +248,9 @@ class XfgBurnMintVerifier:
                          target_chain_id, commitment_version)
         return self.verify_with_public_inputs(proof, air)
 
-    def batch_verify(self, proofs_and_airs, threads=0):
-        """BatchBurnMintVerifier::verify_batch: list of (proof, air) -> list of bool (host threads)"""
+    def batch_verify(self, proofs_and_airs, threads=0, gpu=None):
+        """BatchBurnMintVerifier::verify_batch: list of (proof, air) -> list of bool. Host threads, or
+        the GPU of `gpu` (an XfgBurnMintProver context) via xfg_verify_batch_gpu."""
         k = len(proofs_and_airs)
         if k == 0:
             return []
@@ -257,6 +260,11 @@ class XfgBurnMintVerifier:
         airs = (_AirConsts * k)(*[_air_struct(a) for _, a in proofs_and_airs])
         res = (C.c_int * k)()
         o = self.proof_options._c()
+        if gpu is not None:
+            st = _lib.xfg_verify_batch_gpu(gpu._ctx, k, ptrs, lens, airs, C.byref(o), res)
+            if st:
+                raise gpu._err(st)
+            return [r == 0 for r in res]
         st = _lib.xfg_verify_batch(k, ptrs, lens, airs, C.byref(o), res, threads)
         if st:
             raise XfgStarkError(st, STATUS.get(st))
