@@ -308,14 +308,10 @@ struct xfg_ctx {
     int last_lane = 0;
     // batched GPU verification workspace (xfg_verify_batch_gpu)
     struct {
-        xfg::DBuf<uint8_t> blob;
-        xfg::DBuf<xfg::VGather> g;
-        xfg::DBuf<xfg::VLeaf> lv;
-        xfg::DBuf<uint32_t> rounds, flags;
-        xfg::DBuf<xfg::VFieldProof> fp;
-        xfg::DBuf<xfg::VFieldQuery> fq;
+        xfg::HBuf<uint8_t> stage;  // pinned: proof blob + task lists, one DMA
+        xfg::DBuf<uint8_t> dstage;
+        xfg::DBuf<uint32_t> flags;
         xfg::DBuf<xfg::Digest> dig, rootdig;
-        xfg::DBuf<uint64_t> rootidx;
     } vb;
 };
 
@@ -1563,6 +1559,8 @@ int xfg_verify_batch_gpu(xfg_ctx* c, uint32_t count, const uint8_t* const* proof
     return guarded(c, [&]() -> int {
         HIPCHK(hipSetDevice(c->device));
         const Opts acc = to_opts(acceptable);
+        HostTrace ht;
+        ht.mark("start");
         std::vector<VState> st(count);
         std::vector<std::string> err(count);
         const unsigned nt = std::max(1u, std::min<unsigned>(std::thread::hardware_concurrency(), 16));
@@ -1586,77 +1584,127 @@ int xfg_verify_batch_gpu(xfg_ctx* c, uint32_t count, const uint8_t* const* proof
                 err[i] = std::string("ProofDeserializationError(\"") + e.what() + "\")";
             }
         });
-        // 2. plan: blob of all proofs, Merkle tasks, field queries
-        VerifyPlan plan;
-        std::vector<int> planned(count, -1);
-        size_t total = 0;
-        for (uint32_t i = 0; i < count; i++) total += (proofs[i] ? lens[i] : 0);
-        plan.blob.reserve(total);
-        for (uint32_t i = 0; i < count; i++) {
-            if (!err[i].empty()) continue;
-            const size_t off = plan.blob.size();
-            plan.blob.insert(plan.blob.end(), proofs[i], proofs[i] + lens[i]);
+        ht.mark("transcripts");
+        // 2. plan: per-proof task fragments (local slot numbers) built in parallel; blob offsets by
+        //    prefix sum of the accepted proofs' lengths
+        std::vector<size_t> boff(count + 1, 0);
+        for (uint32_t i = 0; i < count; i++) boff[i + 1] = boff[i] + (err[i].empty() ? lens[i] : 0);
+        std::vector<VerifyPlan> frag(count);
+        parallel([&](uint32_t i) {
+            if (!err[i].empty()) return;
             std::string e;
-            if (plan_proof(st[i], off, plan, e)) planned[i] = (int)plan.roots.size() - 1;
-            else err[i] = e;
+            if (!plan_proof(st[i], boff[i], frag[i], e)) err[i] = e;
+        });
+        ht.mark("plan_fragments");
+        // 3. concatenate into one pinned staging region (parallel fill) and one DMA
+        struct Off {
+            size_t slot = 0, g = 0, lv = 0, q = 0, fp = 0, root = 0;
+            std::vector<size_t> r;
+        };
+        std::vector<Off> fo(count + 1);
+        size_t nrounds = 0;
+        for (uint32_t i = 0; i < count; i++) nrounds = std::max(nrounds, frag[i].rounds.size());
+        std::vector<std::vector<size_t>> rcount(nrounds, std::vector<size_t>(count + 1, 0));
+        std::vector<int> planned(count, -1);
+        int nplanned = 0;
+        for (uint32_t i = 0; i < count; i++) {
+            const bool ok = err[i].empty();
+            const VerifyPlan& f = frag[i];
+            Off& a = fo[i];
+            Off& b = fo[i + 1];
+            b.slot = a.slot + (ok ? f.nslots : 0);
+            b.g = a.g + (ok ? f.gathers.size() : 0);
+            b.lv = a.lv + (ok ? f.leaves.size() : 0);
+            b.q = a.q + (ok ? f.fqueries.size() : 0);
+            b.fp = a.fp + (ok ? 1 : 0);
+            b.root = a.root + (ok ? f.roots[0].size() : 0);
+            for (size_t r = 0; r < nrounds; r++)
+                rcount[r][i + 1] = rcount[r][i] + (ok && r < f.rounds.size() ? f.rounds[r].size() : 0);
+            if (ok) planned[i] = nplanned++;
         }
-        // 3. device work
-        std::vector<u64> ridx;
-        for (auto& rs : plan.roots)
-            for (int64_t r : rs) ridx.push_back(r >= 0 ? (u64)r : 0);
-        std::vector<Digest> rootd(ridx.size());
-        std::vector<uint32_t> flags(plan.fproofs.size(), 0);
-        if (!plan.roots.empty()) {
-            auto& V = c->vb;
-            hipStream_t s = lane0(c)->stream;
-            std::vector<uint32_t> rounds;
-            std::vector<u64> roff{0};
-            for (auto& r : plan.rounds) {
-                rounds.insert(rounds.end(), r.begin(), r.end());
-                roff.push_back(rounds.size());
+        std::vector<size_t> rbase(nrounds + 1, 0);
+        for (size_t r = 0; r < nrounds; r++) rbase[r + 1] = rbase[r] + rcount[r][count];
+        auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+        const size_t o_blob = 0, o_g = al(boff[count]), o_lv = al(o_g + fo[count].g * sizeof(VGather)),
+                     o_r = al(o_lv + fo[count].lv * sizeof(VLeaf)), o_fp = al(o_r + rbase[nrounds] * 4),
+                     o_fq = al(o_fp + fo[count].fp * sizeof(VFieldProof)),
+                     o_ri = al(o_fq + fo[count].q * sizeof(VFieldQuery)), total_b = al(o_ri + fo[count].root * 8);
+        auto& V = c->vb;
+        uint8_t* H = V.stage.ensure(total_b);
+        VGather* hg = (VGather*)(H + o_g);
+        VLeaf* hl = (VLeaf*)(H + o_lv);
+        uint32_t* hr = (uint32_t*)(H + o_r);
+        VFieldProof* hfp = (VFieldProof*)(H + o_fp);
+        VFieldQuery* hfq = (VFieldQuery*)(H + o_fq);
+        u64* hri = (u64*)(H + o_ri);
+        std::vector<int64_t> rootslot(fo[count].root);
+        parallel([&](uint32_t i) {
+            if (boff[i + 1] > boff[i]) memcpy(H + o_blob + boff[i], proofs[i], lens[i]);
+            if (planned[i] < 0) return;
+            const VerifyPlan& f = frag[i];
+            const Off& a = fo[i];
+            const uint32_t sb = (uint32_t)a.slot;
+            for (size_t k = 0; k < f.gathers.size(); k++) {
+                hg[a.g + k] = f.gathers[k];
+                hg[a.g + k].dst += sb;
             }
-            V.blob.ensure(plan.blob.size());
-            V.g.ensure(std::max<size_t>(1, plan.gathers.size()));
-            V.lv.ensure(std::max<size_t>(1, plan.leaves.size()));
-            V.rounds.ensure(std::max<size_t>(1, rounds.size()));
-            V.fp.ensure(plan.fproofs.size());
-            V.fq.ensure(std::max<size_t>(1, plan.fqueries.size()));
-            V.dig.ensure(std::max<uint32_t>(1, plan.nslots));
-            V.flags.ensure(plan.fproofs.size());
-            V.rootidx.ensure(ridx.size());
-            V.rootdig.ensure(ridx.size());
-            HIPCHK(hipMemcpyAsync(V.blob.p, plan.blob.data(), plan.blob.size(), hipMemcpyHostToDevice, s));
-            HIPCHK(hipMemcpyAsync(V.g.p, plan.gathers.data(), plan.gathers.size() * sizeof(VGather), hipMemcpyHostToDevice, s));
-            HIPCHK(hipMemcpyAsync(V.lv.p, plan.leaves.data(), plan.leaves.size() * sizeof(VLeaf), hipMemcpyHostToDevice, s));
-            HIPCHK(hipMemcpyAsync(V.rounds.p, rounds.data(), rounds.size() * 4, hipMemcpyHostToDevice, s));
-            HIPCHK(hipMemcpyAsync(V.fp.p, plan.fproofs.data(), plan.fproofs.size() * sizeof(VFieldProof),
-                                  hipMemcpyHostToDevice, s));
-            HIPCHK(hipMemcpyAsync(V.fq.p, plan.fqueries.data(), plan.fqueries.size() * sizeof(VFieldQuery),
-                                  hipMemcpyHostToDevice, s));
-            HIPCHK(hipMemcpyAsync(V.rootidx.p, ridx.data(), ridx.size() * 8, hipMemcpyHostToDevice, s));
-            HIPCHK(hipMemsetAsync(V.flags.p, 0, plan.fproofs.size() * 4, s));
-            launch_verify(V.blob.p, V.g.p, plan.gathers.size(), V.lv.p, plan.leaves.size(), V.rounds.p, roff.data(),
-                          (int)plan.rounds.size(), V.fp.p, V.fq.p, plan.fqueries.size(), V.dig.p, V.flags.p, s);
-            launch_gather_digest(V.dig.p, V.rootidx.p, V.rootdig.p, ridx.size(), s);
-            HIPCHK(hipMemcpyAsync(rootd.data(), V.rootdig.p, ridx.size() * sizeof(Digest), hipMemcpyDeviceToHost, s));
+            for (size_t k = 0; k < f.leaves.size(); k++) {
+                hl[a.lv + k] = f.leaves[k];
+                hl[a.lv + k].dst += sb;
+            }
+            for (size_t r = 0; r < f.rounds.size(); r++) {
+                uint32_t* d = hr + rbase[r] + rcount[r][i];
+                for (size_t k = 0; k < f.rounds[r].size(); k++) d[k] = f.rounds[r][k] + sb;
+            }
+            hfp[a.fp] = f.fproofs[0];
+            for (size_t k = 0; k < f.fqueries.size(); k++) {
+                hfq[a.q + k] = f.fqueries[k];
+                hfq[a.q + k].proof = (uint32_t)a.fp;
+            }
+            for (size_t t = 0; t < f.roots[0].size(); t++) {
+                const int64_t r = f.roots[0][t];
+                rootslot[a.root + t] = r >= 0 ? r + sb : -1;
+                hri[a.root + t] = r >= 0 ? (u64)(r + sb) : 0;
+            }
+        });
+        ht.mark("plan_merge");
+        std::vector<Digest> rootd(fo[count].root);
+        std::vector<uint32_t> flags(fo[count].fp, 0);
+        if (nplanned > 0) {
+            hipStream_t s = lane0(c)->stream;
+            V.dstage.ensure(total_b);
+            V.dig.ensure(std::max<size_t>(1, fo[count].slot));
+            V.flags.ensure(fo[count].fp);
+            V.rootdig.ensure(fo[count].root);
+            HIPCHK(hipMemcpyAsync(V.dstage.p, H, total_b, hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemsetAsync(V.flags.p, 0, fo[count].fp * 4, s));
+            ht.mark("upload_enqueue");
+            uint8_t* D = V.dstage.p;
+            launch_verify(D + o_blob, (const VGather*)(D + o_g), fo[count].g, (const VLeaf*)(D + o_lv), fo[count].lv,
+                          (const uint32_t*)(D + o_r), rbase.data(), (int)nrounds, (const VFieldProof*)(D + o_fp),
+                          (const VFieldQuery*)(D + o_fq), fo[count].q, V.dig.p, V.flags.p, s);
+            launch_gather_digest(V.dig.p, (const u64*)(D + o_ri), V.rootdig.p, fo[count].root, s);
+            HIPCHK(hipMemcpyAsync(rootd.data(), V.rootdig.p, rootd.size() * sizeof(Digest), hipMemcpyDeviceToHost, s));
             HIPCHK(hipMemcpyAsync(flags.data(), V.flags.p, flags.size() * 4, hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));
+            ht.mark("device");
         }
         // 4. verdicts in the host verifier's check order
-        std::vector<size_t> rbase(plan.roots.size() + 1, 0);
-        for (size_t k = 0; k < plan.roots.size(); k++) rbase[k + 1] = rbase[k] + plan.roots[k].size();
         parallel([&](uint32_t i) {
             if (planned[i] >= 0) {
-                const int k = planned[i];
-                std::vector<Digest> rd(plan.roots[k].size());
-                for (size_t t = 0; t < rd.size(); t++) {
-                    if (plan.roots[k][t] >= 0) rd[t] = rootd[rbase[k] + t];
+                const Off& a = fo[i];
+                const size_t nr = fo[i + 1].root - a.root;
+                std::vector<Digest> rd(nr);
+                for (size_t t = 0; t < nr; t++) {
+                    if (rootslot[a.root + t] >= 0) rd[t] = rootd[a.root + t];
                     else memset(rd[t].w, 0xFF, 32);
                 }
-                err[i] = finish_proof(st[i], rd, flags[plan.fidx[k]]);
+                err[i] = finish_proof(st[i], rd, flags[a.fp]);
             }
             results[i] = proofs[i] ? (err[i].empty() ? XFG_OK : XFG_VERIFY_FAILED) : XFG_INVALID_ARGUMENT;
         });
+        ht.mark("finish");
+        ht.dump((int)count);
         return XFG_OK;
     });
 }

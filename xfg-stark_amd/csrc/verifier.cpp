@@ -125,51 +125,76 @@ std::string parse_proof(const uint8_t* bytes, size_t len, ParsedProof& pf) {
 bool merkle_symbolic(const std::vector<u64>& idx, const Paths& paths, u64 L, MerkleSym& out) {
     BatchOpening plan;
     plan_batch_opening(idx, L, plan);
-    out.given.clear();
-    out.levels.clear();
+    out = MerkleSym();
     if (plan.size() != paths.ptr.size()) return false;
-    std::vector<u64> known;  // heap indices available so far
-    for (u64 i : idx) known.push_back(L + i);
+    const unsigned depth = ilog2(L);
+    // nodes available per level (0 = leaves) as (heap index, slot), sorted before use; per-thread
+    // scratch so batch planning does not allocate per tree
+    thread_local std::vector<std::vector<std::pair<u64, uint32_t>>> lv;
+    if (lv.size() < depth + 1) lv.resize(depth + 1);
+    for (unsigned l = 0; l <= depth; l++) lv[l].clear();
+    uint32_t s = 0;
+    out.leaf_slot.resize(idx.size());
+    for (size_t i = 0; i < idx.size(); i++) {
+        out.leaf_slot[i] = s;
+        lv[0].push_back({L + idx[i], s++});
+    }
     for (size_t i = 0; i < plan.size(); i++) {
         if (paths.cnt[i] != plan.len[i]) return false;
         for (unsigned k = 0; k < plan.len[i]; k++) {
-            out.given.push_back({plan.row(i)[k], paths.ptr[i] + 32 * k});
-            known.push_back(plan.row(i)[k]);
+            const u64 h = plan.row(i)[k];
+            lv[depth - (63 - __builtin_clzll(h))].push_back({h, s});
+            out.given.push_back({s++, paths.ptr[i] + 32 * k});
         }
     }
-    std::sort(known.begin(), known.end());
-    known.erase(std::unique(known.begin(), known.end()), known.end());
-    auto has = [&](u64 h) { return std::binary_search(known.begin(), known.end(), h); };
-    std::vector<u64> level;
-    for (u64 i : idx) level.push_back(L + i);
+    thread_local std::vector<u64> level, up;
+    level.resize(idx.size());
+    for (size_t i = 0; i < idx.size(); i++) level[i] = L + idx[i];
     std::sort(level.begin(), level.end());
     level.erase(std::unique(level.begin(), level.end()), level.end());
-    while (!(level.size() == 1 && level[0] == 1)) {
-        std::vector<u64> up, trip;
+    out.levels.resize(depth);
+    for (unsigned l = 0; l < depth; l++) {
+        auto& cur = lv[l];
+        std::sort(cur.begin(), cur.end());
+        for (size_t i = 1; i < cur.size(); i++)
+            if (cur[i].first == cur[i - 1].first) return false;
+        auto find = [&](u64 h, uint32_t& sl) {
+            auto it = std::lower_bound(cur.begin(), cur.end(), std::make_pair(h, (uint32_t)0));
+            if (it == cur.end() || it->first != h) return false;
+            sl = it->second;
+            return true;
+        };
+        std::vector<uint32_t>& trip = out.levels[l];
+        trip.reserve(3 * level.size());
+        up.clear();
         for (u64 x : level) {
             const u64 p = x >> 1;
             if (!up.empty() && up.back() == p) continue;
-            if (!has(2 * p) || !has(2 * p + 1)) return false;
-            trip.insert(trip.end(), {p, 2 * p, 2 * p + 1});
+            uint32_t a, b;
+            if (!find(2 * p, a) || !find(2 * p + 1, b)) return false;
+            trip.insert(trip.end(), {s, a, b});
+            lv[l + 1].push_back({p, s++});
             up.push_back(p);
         }
-        for (u64 p : up) known.insert(std::upper_bound(known.begin(), known.end(), p), p);
-        out.levels.push_back(std::move(trip));
         level.swap(up);
     }
+    if (level.size() != 1 || level[0] != 1) return false;
+    out.root = lv[depth].back().second;  // the last node added at the top level is the root
+    for (auto& e : lv[depth])
+        if (e.first == 1) out.root = e.second;
+    out.nslots = s;
     return true;
 }
 static bool batch_root(const std::vector<u64>& idx, const std::vector<Digest>& leaf, const Paths& paths, u64 L,
                        Digest& root) {
     MerkleSym sym;
     if (!merkle_symbolic(idx, paths, L, sym)) return false;
-    std::unordered_map<u64, Digest> val;
-    val.reserve(2 * (sym.given.size() + idx.size()) + 64);
-    for (size_t i = 0; i < idx.size(); i++) val[L + idx[i]] = leaf[i];
+    std::vector<Digest> val(sym.nslots);
+    for (size_t i = 0; i < idx.size(); i++) val[sym.leaf_slot[i]] = leaf[i];
     for (auto& g : sym.given) memcpy(val[g.first].w, g.second, 32);
-    for (auto& lv : sym.levels)
-        for (size_t t = 0; t < lv.size(); t += 3) val[lv[t]] = b3_merge(val[lv[t + 1]], val[lv[t + 2]]);
-    root = val[1];
+    for (auto& lvl : sym.levels)
+        for (size_t t = 0; t < lvl.size(); t += 3) val[lvl[t]] = b3_merge(val[lvl[t + 1]], val[lvl[t + 2]]);
+    root = val[sym.root];
     return true;
 }
 static bool same(const Digest& a, const Digest& b) { return !memcmp(a.w, b.w, 32); }
@@ -456,29 +481,15 @@ bool plan_proof(const VState& st, size_t blob_off, VerifyPlan& plan, std::string
                         uint32_t words) -> int64_t {
         MerkleSym sym;
         if (!merkle_symbolic(idx, paths, L, sym)) return -1;
-        std::unordered_map<u64, uint32_t> slot;
-        slot.reserve(2 * (idx.size() + sym.given.size()) + 64);
-        for (size_t i = 0; i < idx.size(); i++) {
-            const uint32_t sl = plan.nslots++;
-            slot[L + idx[i]] = sl;
-            plan.leaves.push_back(VLeaf{off(leaf0 + i * stride), words, sl});
-        }
-        for (auto& g : sym.given) {
-            const uint32_t sl = plan.nslots++;
-            slot[g.first] = sl;
-            plan.gathers.push_back(VGather{off(g.second), sl, 0});
-        }
+        const uint32_t b = plan.nslots;
+        for (size_t i = 0; i < idx.size(); i++)
+            plan.leaves.push_back(VLeaf{off(leaf0 + i * stride), words, b + sym.leaf_slot[i]});
+        for (auto& g : sym.given) plan.gathers.push_back(VGather{off(g.second), b + g.first, 0});
         if (plan.rounds.size() < sym.levels.size()) plan.rounds.resize(sym.levels.size());
-        for (size_t r = 0; r < sym.levels.size(); r++) {
-            const auto& lv = sym.levels[r];
-            for (size_t t = 0; t < lv.size(); t += 3) {
-                const uint32_t sl = plan.nslots++;
-                const uint32_t a = slot[lv[t + 1]], b = slot[lv[t + 2]];
-                slot[lv[t]] = sl;
-                plan.rounds[r].insert(plan.rounds[r].end(), {sl, a, b});
-            }
-        }
-        return slot[1];
+        for (size_t r = 0; r < sym.levels.size(); r++)
+            for (uint32_t x : sym.levels[r]) plan.rounds[r].push_back(b + x);
+        plan.nslots += sym.nslots;
+        return (int64_t)(b + sym.root);
     };
     roots.push_back(add_tree(st.pos, pf.trace_paths, N, pf.trace_rows.p, 56, 7));
     roots.push_back(add_tree(st.pos, pf.constraint_paths, N, pf.constraint_rows.p, 8 * de, (uint32_t)de));

@@ -59,11 +59,14 @@ std::string verify_transcript(const uint8_t* bytes, size_t len, const AirConst& 
 // the query checks on the host (Merkle openings, DEEP, FRI, remainder)
 std::string verify_queries_host(const VState& st);
 
-// symbolic BatchMerkleProof::get_root: which heap nodes the proof provides and which are merged,
-// level by level (parent, left, right); false when the node vectors do not fit the opening plan
+// symbolic BatchMerkleProof::get_root over local digest slots: slots of the queried leaves, the
+// digests the proof provides, and the merges level by level (out, left, right); false when the node
+// vectors do not fit the opening plan
 struct MerkleSym {
-    std::vector<std::pair<u64, const uint8_t*>> given;  // heap index, digest bytes in the proof
-    std::vector<std::vector<u64>> levels;               // per level: parent, left, right, ...
+    uint32_t nslots = 0, root = 0;
+    std::vector<uint32_t> leaf_slot;                         // per queried leaf
+    std::vector<std::pair<uint32_t, const uint8_t*>> given;  // slot, digest bytes in the proof
+    std::vector<std::vector<uint32_t>> levels;               // per level: out, left, right slots
 };
 bool merkle_symbolic(const std::vector<u64>& idx, const Paths& paths, u64 L, MerkleSym& out);
 

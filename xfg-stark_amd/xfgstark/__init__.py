@@ -251,13 +251,16 @@ class XfgBurnMintVerifier:
     def batch_verify(self, proofs_and_airs, threads=0, gpu=None):
         """BatchBurnMintVerifier::verify_batch: list of (proof, air) -> list of bool. Host threads, or
         the GPU of `gpu` (an XfgBurnMintProver context) via xfg_verify_batch_gpu."""
+        import numpy as np
         k = len(proofs_and_airs)
         if k == 0:
             return []
         datas = [(p.to_bytes() if isinstance(p, StarkProof) else bytes(p)) for p, _ in proofs_and_airs]
+        # statements as one numpy array (per-item ctypes structs dominated large batches)
         ptrs = (_u8p * k)(*[_bytes_ptr(d) for d in datas])
         lens = (C.c_size_t * k)(*[len(d) for d in datas])
-        airs = (_AirConsts * k)(*[_air_struct(a) for _, a in proofs_and_airs])
+        air_np = np.array([list(a[0]) + [a[1], a[2]] for _, a in proofs_and_airs], dtype=np.uint64)
+        airs = air_np.ctypes.data_as(C.POINTER(_AirConsts))
         res = (C.c_int * k)()
         o = self.proof_options._c()
         if gpu is not None:
