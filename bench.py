@@ -121,6 +121,38 @@ def pipelined_steps(submit_fn, collect_fn, batches, rank, world, per_rank, devic
     return gather_proofs(collect_fn(pending), rank, world, per_rank, device, dist)
 
 
+def config5(prover, batch=4, calls=5):
+    """side measurement of BASELINE configs[4]: 2^20-step trace, blowup 16, 96-bit class options
+    (quadratic extension, 24 queries, grinding 4), batches of `batch` proofs per call on this GPU"""
+    import xfgstark
+    n5 = 1 << 20
+    o = xfgstark.ProofOptions.reference()
+    o.field_extension, o.blowup_factor, o.num_queries = 2, 16, 24
+    saved = prover._options
+    prover._options = o
+    try:
+        prover.prepare(batch, n5)
+        kws = [synthetic.burn_inputs(50_000 + i) for i in range(batch)]
+        pend = None
+        t = time.perf_counter()
+        for _ in range(calls):
+            nxt = prover.submit_batch(kws, trace_length=n5)
+            if pend is not None:
+                pend.result()
+            pend = nxt
+        res = pend.result()
+        dt = time.perf_counter() - t
+        assert all(not isinstance(r, Exception) for r in res)
+        lde_ms = prover.bench_lde(1, n5, 16, 5)
+    finally:
+        prover._options = saved
+    return {"workload": "configs[4]: 2^20-step trace, blowup 16, quadratic extension, 24 queries, grinding 4",
+            "proofs_per_call": batch, "proofs_per_s": round(batch * calls / dt, 2),
+            "ms_per_proof": round(dt / (batch * calls) * 1e3, 3), "proof_bytes": len(res[0]),
+            "trace_lde_ms": round(lde_ms, 3),
+            "trace_lde_GBps": round(8 * WIDTH * (n5 + 16 * n5) / (lde_ms * 1e-3) / 1e9, 1)}
+
+
 def pmc_traffic(per, n, blowup):
     """HBM bytes per trace-LDE launch set from the committed PMC pass (profiles/rNN/lde_pmc.json,
     made by scripts/profile_round.sh: FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 --pmc runs)"""
@@ -162,6 +194,7 @@ def main():
     ap.add_argument("--log-n", type=int, default=LOG_N)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-config5", action="store_true", help="skip the configs[4] side measurement")
     args = ap.parse_args()
 
     import torch
@@ -239,6 +272,7 @@ def main():
         prover.prove_batch([synthetic.burn_inputs(i) for i in range(per)], trace_length=n)
         prover_stage = {k: round(v, 3) for k, v in prover.stage_times().items()}
     prover.set_timing(False)
+    c5 = None if (args.no_config5 or rank != 0) else config5(prover)
 
     if rank == 0:
         total = per * world * args.steps
@@ -270,6 +304,8 @@ def main():
             "stage_ms_one_batch": prover_stage,
             "sync_prove_batch_ms": round(sync_call_ms, 3),
         }
+        if c5:
+            line["config5"] = c5
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(line), flush=True)

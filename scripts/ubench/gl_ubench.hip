@@ -22,6 +22,34 @@ __device__ __forceinline__ u64 add_asm(u64 a, u64 b) {
         : "vcc");
     return (u64)dl | ((u64)dh << 32);
 }
+// carries in compiler-allocated SGPR pairs (not VCC), so independent adds can interleave
+__device__ __forceinline__ u64 add_sg(u64 a, u64 b) {
+    u32 al = (u32)a, ah = (u32)(a >> 32), bl = (u32)b, bh = (u32)(b >> 32), ql, qh, dl, dh, e;
+    u64 c0, c1, c2, c3;
+    asm volatile(
+        "v_sub_co_u32_e64 %[ql], %[c0], 1, %[bl]\n\t"
+        "v_subb_co_u32_e64 %[qh], %[c1], -1, %[bh], %[c0]\n\t"
+        "v_sub_co_u32_e64 %[dl], %[c2], %[al], %[ql]\n\t"
+        "v_subb_co_u32_e64 %[dh], %[c3], %[ah], %[qh], %[c2]\n\t"
+        "v_cndmask_b32_e64 %[e], 0, -1, %[c3]\n\t"
+        : [ql] "=&v"(ql), [qh] "=&v"(qh), [dl] "=&v"(dl), [dh] "=&v"(dh), [e] "=&v"(e), [c0] "=&s"(c0),
+          [c1] "=&s"(c1), [c2] "=&s"(c2), [c3] "=&s"(c3)
+        : [al] "v"(al), [ah] "v"(ah), [bl] "v"(bl), [bh] "v"(bh));
+    u64 d = (u64)dl | ((u64)dh << 32);
+    return d - (u64)e;  // borrowed: a + b = d - EPS (mod 2^64); e = EPS or 0
+}
+__device__ __forceinline__ u64 sub_sg(u64 a, u64 b) {
+    u32 al = (u32)a, ah = (u32)(a >> 32), bl = (u32)b, bh = (u32)(b >> 32), dl, dh, e;
+    u64 c0, c1;
+    asm volatile(
+        "v_sub_co_u32_e64 %[dl], %[c0], %[al], %[bl]\n\t"
+        "v_subb_co_u32_e64 %[dh], %[c1], %[ah], %[bh], %[c0]\n\t"
+        "v_cndmask_b32_e64 %[e], 0, -1, %[c1]\n\t"
+        : [dl] "=&v"(dl), [dh] "=&v"(dh), [e] "=&v"(e), [c0] "=&s"(c0), [c1] "=&s"(c1)
+        : [al] "v"(al), [ah] "v"(ah), [bl] "v"(bl), [bh] "v"(bh));
+    u64 d = (u64)dl | ((u64)dh << 32);
+    return d - (u64)e;
+}
 __device__ __forceinline__ u64 sub_asm(u64 a, u64 b) {
     u32 al = (u32)a, ah = (u32)(a >> 32), bl = (u32)b, bh = (u32)(b >> 32), dl, dh, e;
     asm volatile(
@@ -97,6 +125,8 @@ KERNEL(k_add_asm, add_asm)
 KERNEL(k_sub_c, gl_sub)
 KERNEL(k_sub_asm, sub_asm)
 KERNEL(k_mul_c, gl_mul)
+KERNEL(k_add_sg, add_sg)
+KERNEL(k_sub_sg, sub_sg)
 KERNEL(k_mul_asm, mul_asm)
 
 static u64 rnd(u64& s) {
@@ -136,7 +166,8 @@ int main() {
         int kind;
     } ks[] = {{"add C", k_add_c, k_add_c_one, 0},   {"add asm", k_add_asm, k_add_asm_one, 0},
               {"sub C", k_sub_c, k_sub_c_one, 1},   {"sub asm", k_sub_asm, k_sub_asm_one, 1},
-              {"mul C", k_mul_c, k_mul_c_one, 2},   {"mul asm", k_mul_asm, k_mul_asm_one, 2}};
+              {"mul C", k_mul_c, k_mul_c_one, 2},   {"mul asm", k_mul_asm, k_mul_asm_one, 2},
+              {"add sg", k_add_sg, k_add_sg_one, 0}, {"sub sg", k_sub_sg, k_sub_sg_one, 1}};
     for (auto& kk : ks) {
         hipLaunchKernelGGL(kk.one, dim3(N / 256), dim3(256), 0, 0, da, db, dout, N);
         hipMemcpy(ho, dout, N * 8, hipMemcpyDeviceToHost);

@@ -44,7 +44,8 @@ def with_blowup(prover, b):
     return o
 
 
-@pytest.mark.parametrize("n,blowup", [(8, 2), (64, 8), (256, 16), (1024, 4), (4096, 8), (1 << 15, 8)])
+@pytest.mark.parametrize("n,blowup", [(8, 2), (64, 8), (256, 16), (1024, 4), (4096, 8), (1 << 15, 8), (1 << 16, 2),
+                                      (1 << 17, 2), (1 << 20, 2)])
 def test_lde_kernel_matches_oracle(prover, n, blowup):
     rng = np.random.default_rng(n + blowup)
     coef = rng.integers(0, P, size=(3, n), dtype=np.uint64)
@@ -54,7 +55,8 @@ def test_lde_kernel_matches_oracle(prover, n, blowup):
         assert [int(v) for v in got[p]] == want
 
 
-@pytest.mark.parametrize("n,off7", [(8, False), (64, True), (2048, False), (2048, True), (1 << 14, True)])
+@pytest.mark.parametrize("n,off7", [(8, False), (64, True), (2048, False), (2048, True), (1 << 14, True),
+                                    (1 << 17, True), (1 << 20, False)])
 def test_interpolate_kernel_matches_oracle(prover, n, off7):
     rng = np.random.default_rng(n)
     ev = rng.integers(0, P, size=(2, n), dtype=np.uint64)

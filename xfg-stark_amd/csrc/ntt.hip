@@ -288,19 +288,42 @@ static void run_pass_a(int logR, dim3 g, size_t lds, hipStream_t s, const NttArg
 }
 template <bool INV>
 static void run_pass_b(int logC, dim3 g, size_t lds, hipStream_t s, const NttArgs& a) {
-#define XFG_CASE_B(L) \
-    case L: hipLaunchKernelGGL((ntt_pass_b<L, INV>), g, dim3(THREADS), lds, s, a); break;
+    // C = 4096 rows need 67 KiB of LDS (a workgroup may use up to 160 KiB on gfx950)
+#define XFG_CASE_B(L)                                                                                         \
+    case L:                                                                                                   \
+        if (lds > 65536) {                                                                                    \
+            static const bool ok_ = hipFuncSetAttribute((const void*)ntt_pass_b<L, INV>,                      \
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize,           \
+                                                        160 * 1024) == hipSuccess;                            \
+            (void)ok_;                                                                                        \
+        }                                                                                                     \
+        hipLaunchKernelGGL((ntt_pass_b<L, INV>), g, dim3(THREADS), lds, s, a);                                \
+        break;
     switch (logC) {
         XFG_CASE_B(2) XFG_CASE_B(3) XFG_CASE_B(4) XFG_CASE_B(5) XFG_CASE_B(6) XFG_CASE_B(7)
-        XFG_CASE_B(8) XFG_CASE_B(9) XFG_CASE_B(10) XFG_CASE_B(11)
+        XFG_CASE_B(8) XFG_CASE_B(9) XFG_CASE_B(10) XFG_CASE_B(11) XFG_CASE_B(12)
         default: break;
     }
 #undef XFG_CASE_B
 }
 
 static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
-    a.logR = a.logn / 2;
-    a.logC = a.logn - a.logR;
+    // split n = R * C: evenly below 2^18, C = 2R from 2^18 on (faster at 2^18 and 2^20, see
+    // scripts/ntt_split.py); XFG_NTT_LOGC forces log2(C) for tuning sweeps
+    static const int force_logc = [] {
+        const char* v = getenv("XFG_NTT_LOGC");
+        return v && *v ? atoi(v) : 0;
+    }();
+    if (force_logc > 1 && force_logc <= 12 && a.logn - force_logc >= 1 && a.logn - force_logc <= 10) {
+        a.logC = force_logc;
+        a.logR = a.logn - a.logC;
+    } else if (a.logn >= 18) {  // measured (scripts/ntt_split.py): C one step wider than R at 2^18 / 2^20
+        a.logC = a.logn / 2 + 1;
+        a.logR = a.logn - a.logC;
+    } else {
+        a.logR = a.logn / 2;
+        a.logC = a.logn - a.logR;
+    }
     const int R = 1 << a.logR, C = 1 << a.logC;
     const int logTC = a.logC < 12 - a.logR ? a.logC : 12 - a.logR;
     const int logTR = a.logR < 12 - a.logC ? a.logR : 12 - a.logC;
