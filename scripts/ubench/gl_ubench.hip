@@ -103,6 +103,39 @@ __device__ __forceinline__ u64 mul_asm(u64 a, u64 b) {
     return reduce_asm(hi, lo);
 }
 
+// C forms with the carries taken from __builtin_*_overflow (the compiler keeps them in SGPR pairs)
+__device__ __forceinline__ u64 add_v6(u64 a, u64 b) {
+    // a, b < p: s = a + b; s >= p iff carry or s + EPS carries
+    u64 s, t;
+    const bool c1 = __builtin_add_overflow(a, b, &s);
+    const bool c2 = __builtin_add_overflow(s, EPS, &t);
+    return (c1 | c2) ? t : s;
+}
+__device__ __forceinline__ u64 sub_v5(u64 a, u64 b) {
+    u64 d;
+    const bool c = __builtin_sub_overflow(a, b, &d);
+    return c ? d - EPS : d;
+}
+__device__ __forceinline__ u64 reduce_v(u64 hi, u64 lo) {
+    const u64 hh = hi >> 32, hl = hi & EPS;
+    u64 t0, t2, u;
+    const bool b = __builtin_sub_overflow(lo, hh, &t0);
+    t0 = b ? t0 - EPS : t0;
+    const u64 t1 = (hl << 32) - hl;
+    const bool c = __builtin_add_overflow(t0, t1, &t2);
+    const bool c2 = __builtin_add_overflow(t2, EPS, &u);
+    return (c | c2) ? u : t2;
+}
+__device__ __forceinline__ u64 mul_v(u64 a, u64 b) {
+    const u32 a0 = (u32)a, a1 = (u32)(a >> 32), b0 = (u32)b, b1 = (u32)(b >> 32);
+    const u64 p00 = (u64)a0 * b0;
+    const u64 t1 = (u64)a0 * b1 + (p00 >> 32);
+    const u64 t2 = (u64)a1 * b0 + (u32)t1;
+    const u64 lo = (u64)(u32)p00 | ((u64)(u32)t2 << 32);
+    const u64 hi = (u64)a1 * b1 + ((t1 >> 32) + (t2 >> 32));
+    return reduce_v(hi, lo);
+}
+
 #define KERNEL(NAME, OP)                                                                      \
     __global__ __launch_bounds__(256) void NAME(const u64* in, u64* out, int iters) {         \
         size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;                              \
@@ -128,6 +161,9 @@ KERNEL(k_mul_c, gl_mul)
 KERNEL(k_add_sg, add_sg)
 KERNEL(k_sub_sg, sub_sg)
 KERNEL(k_mul_asm, mul_asm)
+KERNEL(k_add_v6, add_v6)
+KERNEL(k_sub_v5, sub_v5)
+KERNEL(k_mul_v, mul_v)
 
 static u64 rnd(u64& s) {
     s += 0x9E3779B97F4A7C15ULL;
@@ -167,7 +203,9 @@ int main() {
     } ks[] = {{"add C", k_add_c, k_add_c_one, 0},   {"add asm", k_add_asm, k_add_asm_one, 0},
               {"sub C", k_sub_c, k_sub_c_one, 1},   {"sub asm", k_sub_asm, k_sub_asm_one, 1},
               {"mul C", k_mul_c, k_mul_c_one, 2},   {"mul asm", k_mul_asm, k_mul_asm_one, 2},
-              {"add sg", k_add_sg, k_add_sg_one, 0}, {"sub sg", k_sub_sg, k_sub_sg_one, 1}};
+              {"add sg", k_add_sg, k_add_sg_one, 0}, {"sub sg", k_sub_sg, k_sub_sg_one, 1},
+              {"add v6", k_add_v6, k_add_v6_one, 0}, {"sub v5", k_sub_v5, k_sub_v5_one, 1},
+              {"mul v", k_mul_v, k_mul_v_one, 2}};
     for (auto& kk : ks) {
         hipLaunchKernelGGL(kk.one, dim3(N / 256), dim3(256), 0, 0, da, db, dout, N);
         hipMemcpy(ho, dout, N * 8, hipMemcpyDeviceToHost);

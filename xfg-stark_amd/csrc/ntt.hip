@@ -24,18 +24,17 @@
 namespace xfg {
 
 // ---------------------------------------------------------------- shift-based multiplies
-// x * 2^s mod p for 0 <= s < 192 (2^96 == -1); s is a compile-time constant after unrolling
+// x * 2^s mod p for 0 <= s < 96 (2^96 == -1 is handled by the caller); s is a compile-time
+// constant after unrolling. Canonical result for canonical x.
 __device__ __forceinline__ u64 mul_pow2(u64 x, int s) {
-    bool neg = s >= 96;
-    if (neg) s -= 96;
-    u64 r;
-    if (s == 0) r = x;
-    else if (s < 64) r = gl_reduce(x >> (64 - s), x << s);
-    else {
-        u64 y = gl_reduce(x >> (96 - s), x << (s - 32));
-        r = gl_reduce(y >> 32, y << 32);
-    }
-    return neg ? gl_neg(r) : r;
+    if (s == 0) return x;
+    if (s <= 32) return gl_add_small(x << s, ((x >> (64 - s)) << 32) - (x >> (64 - s)));  // hi < 2^32: lo + hi * EPS
+    if (s < 64) return gl_reduce(x >> (64 - s), x << s);
+    // x * 2^(s-64) = v + y * 2^32 with v < 2^32, y = x >> (96 - s) < 2^63; times 2^64 == v * EPS - y
+    const u64 v = (u64)(uint32_t)(x << (s - 64)), y = x >> (96 - s);
+    u64 d;
+    const bool b = __builtin_sub_overflow((v << 32) - v, y, &d);
+    return b ? d - EPS : d;
 }
 // exponent of two of w_{2^k} (Winterfell's roots: get_root_of_unity(k))
 __host__ __device__ constexpr int root_exp2(int k) {
@@ -62,10 +61,15 @@ __device__ __forceinline__ void dft_reg(u64* v) {
             const int pos = b & (h - 1), i0 = ((b >> s) << (s + 1)) + pos;
             int e = (root_exp2(s + 1) * pos) % 192;
             if (INV && e) e = 192 - e;
-            u64 t = mul_pow2(a[i0 + h], e);
-            u64 u = a[i0];
-            a[i0] = gl_add(u, t);
-            a[i0 + h] = gl_sub(u, t);
+            // w = 2^e = -2^(e - 96) for e >= 96: the sign swaps the butterfly's add and sub
+            const u64 t = mul_pow2(a[i0 + h], e % 96), u = a[i0];
+            if (e >= 96) {
+                a[i0] = gl_sub(u, t);
+                a[i0 + h] = gl_add(u, t);
+            } else {
+                a[i0] = gl_add(u, t);
+                a[i0 + h] = gl_sub(u, t);
+            }
         }
     }
 #pragma unroll
