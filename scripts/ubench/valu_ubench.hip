@@ -31,6 +31,30 @@ DEF(k_sdwa_xor, "v_xor_b32_sdwa %0, %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRES
 DEF(k_sdwa_add, "v_add_u32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD")
 DEF(k_cndmask, "v_cndmask_b32_e32 %0, %0, %1, vcc")
 DEF(k_lshrrev, "v_lshrrev_b32_e32 %0, 7, %0")
+// 64-bit register-pair forms (Goldilocks add / compare / multiply lowering)
+#define DEF64(NAME, ASM)                                                                         \
+    __global__ __launch_bounds__(256) void NAME(unsigned* out, int iters) {                    \
+        unsigned long long a0 = threadIdx.x, a1 = a0 * 3, a2 = a0 * 5, a3 = a0 * 7, a4 = a0 + 1,  \
+                           a5 = a0 + 2, a6 = a0 + 3, a7 = a0 + 4, k = blockIdx.x | 1;           \
+        unsigned k32 = blockIdx.x | 1;                                                            \
+        for (int it = 0; it < iters; it++) {                                                     \
+            REP8(asm volatile(ASM : "+v"(a0) : "v"(k), "v"(k32) : "vcc"); asm volatile(ASM : "+v"(a1) : "v"(k), "v"(k32) : "vcc"); \
+                 asm volatile(ASM : "+v"(a2) : "v"(k), "v"(k32) : "vcc"); asm volatile(ASM : "+v"(a3) : "v"(k), "v"(k32) : "vcc"); \
+                 asm volatile(ASM : "+v"(a4) : "v"(k), "v"(k32) : "vcc"); asm volatile(ASM : "+v"(a5) : "v"(k), "v"(k32) : "vcc"); \
+                 asm volatile(ASM : "+v"(a6) : "v"(k), "v"(k32) : "vcc"); asm volatile(ASM : "+v"(a7) : "v"(k), "v"(k32) : "vcc");) \
+        }                                                                                        \
+        out[blockIdx.x * blockDim.x + threadIdx.x] = (unsigned)(a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7); \
+    }
+DEF64(k_lshladd64, "v_lshl_add_u64 %0, %0, 0, %1")
+DEF64(k_cmp64, "v_cmp_lt_u64_e32 vcc, %0, %1")
+DEF64(k_mad64, "v_mad_u64_u32 %0, vcc, %2, %2, %0")
+DEF64(k_lshl64, "v_lshlrev_b64 %0, 7, %0")
+DEF64(k_mov64, "v_mov_b64 %0, %1")
+DEF(k_subco, "v_sub_co_u32_e64 %0, vcc, %0, %1")
+DEF(k_subb, "v_subb_co_u32_e32 %0, vcc, %0, %1, vcc")
+DEF(k_cnd64, "v_cndmask_b32_e64 %0, %0, %1, vcc")
+DEF(k_mov, "v_mov_b32 %0, %1")
+
 int main() {
     unsigned* d;
     const int blocks = 256 * 8, threads = 256, iters = 2048;
@@ -40,7 +64,9 @@ int main() {
         {"v_xad_u32", k_xad}, {"v_bitop3_b32", k_bitop3}, {"v_perm_b32", k_perm}, {"v_mad_u32_u24", k_mad32},
         {"v_mul_lo_u32", k_mullo}, {"v_mul_hi_u32", k_mulhi}, {"v_add_co_u32", k_addco}, {"v_lshl_or_b32", k_lshl_or},
         {"v_xor_b32_sdwa", k_sdwa_xor}, {"v_add_u32_sdwa", k_sdwa_add}, {"v_cndmask_b32", k_cndmask},
-        {"v_lshrrev_b32", k_lshrrev}};
+        {"v_lshrrev_b32", k_lshrrev}, {"v_lshl_add_u64", k_lshladd64}, {"v_cmp_lt_u64", k_cmp64},
+        {"v_mad_u64_u32", k_mad64}, {"v_lshlrev_b64", k_lshl64}, {"v_mov_b64", k_mov64}, {"v_sub_co_u32_e64", k_subco},
+        {"v_subb_co_u32", k_subb}, {"v_cndmask_b32_e64", k_cnd64}, {"v_mov_b32", k_mov}};
     for (auto& k : ks) {
         hipEvent_t a, b;
         hipEventCreate(&a);

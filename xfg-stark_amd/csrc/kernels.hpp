@@ -26,17 +26,29 @@ struct DeepParams {
     u64 pad[2];
 };
 
+// precomputed four-step twiddles (ntt.hip build_fourstep): fwd[logn][logbeta] holds
+// 7^j2 w_N^(j2 (t + beta k1)) at [t][k1][j2], inv[logn] holds w_n^-(j2 k1) / n at [k1][j2];
+// nullptr -> the kernels form them as running products
+constexpr int FOURSTEP_MAX_LOG = 22;
+struct FourStep {
+    const u64* fwd[FOURSTEP_MAX_LOG + 1][5] = {};
+    const u64* inv[FOURSTEP_MAX_LOG + 1] = {};
+};
 struct Tables {
     const u64* tw;     // tw[e] = w_{2^LM}^e, e < 2^LM
     int LM;
     const u64* pow7;   // 7^j,  j < 2^LM
     const u64* ipow7;  // 7^-j, j < 2^LM
+    const FourStep* fs;  // host-side table registry (never dereferenced on the device)
 };
 
 // ---- NTT (four-step, natural order in/out) ----
 // forward LDE: coef[poly][n] -> out[poly][beta][n] (coset-major: out[p][t][m] = P(7 w_N^(t + beta m)))
 void launch_lde(const u64* coef, u64 coef_stride, u64* out, u64* scratch, int npoly, int logn, int logbeta,
                 const Tables& T, hipStream_t s);
+// entries of the four-step table for (logn, logbeta) (inverse: logbeta = -1), and its generator
+u64 fourstep_size(int logn, int logbeta);
+void build_fourstep(u64* out, int logn, int logbeta, const Tables& T, hipStream_t s);
 // inverse: evals[poly][n] at 7^off7 * w_n^i -> coefficients (first `keep` written, stride out_stride)
 void launch_interpolate(const u64* evals, u64 in_stride, u64* out, u64 out_stride, u64* scratch, int npoly, int logn,
                         bool off7, u64 keep, const Tables& T, hipStream_t s);

@@ -96,8 +96,9 @@ __device__ __forceinline__ u64 tw_get(const Tables& T, int k, u64 e, bool inv) {
 // ld(seq, i) reads logical element i of a sequence; st(seq, base, stride, v) receives the R
 // outputs of a group, which belong at logical positions base + r * stride.
 // IN_PLACE: every load of the step completes (barrier) before any store.
-template <int LOGS, int LOGR, bool INV, bool SEQ_FAST, bool IN_PLACE, class LD, class ST>
-__device__ __forceinline__ void stockham(int lognseq, int Ns, const u64* ltw, LD ld, ST st) {
+// pf(q, seq, base, stride) runs before the group's loads (prefetch of what st will need).
+template <int LOGS, int LOGR, bool INV, bool SEQ_FAST, bool IN_PLACE, class LD, class ST, class PF>
+__device__ __forceinline__ void stockham(int lognseq, int Ns, const u64* ltw, LD ld, ST st, PF pf) {
     constexpr int S = 1 << LOGS, R = 1 << LOGR, G = S / R, PER = 16 / R;
     const int nseq = 1 << lognseq;
     const int groups = nseq * G;
@@ -111,6 +112,7 @@ __device__ __forceinline__ void stockham(int lognseq, int Ns, const u64* ltw, LD
         if (g < groups) {
             const int seq = SEQ_FAST ? (g & (nseq - 1)) : (g / G);
             const int j = SEQ_FAST ? (g >> lognseq) : (g % G);
+            pf(q, seq, (j / Ns) * Ns * R + (j % Ns), Ns);
 #pragma unroll
             for (int r = 0; r < R; r++) v[q][r] = ld(seq, j + r * G);
             if (Ns > 1) {
@@ -128,7 +130,7 @@ __device__ __forceinline__ void stockham(int lognseq, int Ns, const u64* ltw, LD
     for (int q = 0; q < PER; q++) {
         if (gs[q] >= 0) {
             const int j = gj[q];
-            st(gs[q], (j / Ns) * Ns * R + (j % Ns), Ns, v[q]);
+            st(q, gs[q], (j / Ns) * Ns * R + (j % Ns), Ns, v[q]);
         }
     }
 }
@@ -145,35 +147,39 @@ struct Plan {
 
 // Whole DFT of every sequence: the first step loads with ldg (global), middle steps run in the
 // LDS tile, the last step stores with stg (global). A one-step DFT goes global -> global.
-template <int LOGS, bool INV, bool FIRST_SEQ_FAST, class LDG, class STG>
-__device__ __forceinline__ void pass_dft(u64* tile, int lognseq, const u64* ltw, LDG ldg, STG stg) {
+// stg(q, seq, base, stride, v) stores group q's outputs; pf as in stockham, for the last step
+template <int LOGS, bool INV, bool FIRST_SEQ_FAST, class LDG, class STG, class PF>
+__device__ __forceinline__ void pass_dft(u64* tile, int lognseq, const u64* ltw, LDG ldg, STG stg, PF pf) {
     using PL = Plan<LOGS>;
     constexpr int PITCH = row_pitch(1 << LOGS);
+    auto nopf = [](int, int, int, int) {};
     if constexpr (PL::NSTEP == 1) {
-        stockham<LOGS, PL::FIRST_LOGR, INV, FIRST_SEQ_FAST, false>(lognseq, 1, ltw, ldg, stg);
+        stockham<LOGS, PL::FIRST_LOGR, INV, FIRST_SEQ_FAST, false>(lognseq, 1, ltw, ldg, stg, pf);
     } else {
         stockham<LOGS, PL::FIRST_LOGR, INV, FIRST_SEQ_FAST, false>(
-            lognseq, 1, ltw, ldg, [&](int seq, int base, int stride, u64* v) {
+            lognseq, 1, ltw, ldg, [&](int, int seq, int base, int stride, u64* v) {
                 u64* row = tile + seq * PITCH;
 #pragma unroll
                 for (int r = 0; r < (1 << PL::FIRST_LOGR); r++) row[phys(base + r * stride)] = v[r];
-            });
+            },
+            nopf);
         __syncthreads();
         int Ns = 1 << PL::FIRST_LOGR;
 #pragma unroll
         for (int st = 1; st < PL::NSTEP - 1; st++) {
             stockham<LOGS, 4, INV, true, true>(
                 lognseq, Ns, ltw, [&](int seq, int i) { return tile[seq * PITCH + phys(i)]; },
-                [&](int seq, int base, int stride, u64* v) {
+                [&](int, int seq, int base, int stride, u64* v) {
                     u64* row = tile + seq * PITCH;
 #pragma unroll
                     for (int r = 0; r < 16; r++) row[phys(base + r * stride)] = v[r];
-                });
+                },
+                nopf);
             __syncthreads();
             Ns <<= 4;
         }
         stockham<LOGS, 4, INV, true, false>(lognseq, Ns, ltw,
-                                            [&](int seq, int i) { return tile[seq * PITCH + phys(i)]; }, stg);
+                                            [&](int seq, int i) { return tile[seq * PITCH + phys(i)]; }, stg, pf);
         __syncthreads();
     }
 }
@@ -188,6 +194,7 @@ struct NttArgs {
     int off7;     // inverse: scale coefficient k by 7^-k
     u64 scale;    // inverse: n^-1
     u64 keep;     // inverse: coefficients written
+    const u64* t4;  // four-step twiddle table (FourStep) or nullptr
     Tables T;
 };
 
@@ -223,8 +230,23 @@ __global__ __launch_bounds__(THREADS) void ntt_pass_a(NttArgs a) {
         u64 v = in[((u64)j1 << a.logC) + col0 + seq];
         return INV ? v : gl_mul(v, pre[j1]);
     };
-    auto stg = [&](int seq, int base, int stride, u64* v) {
+    // four-step twiddles from the table: loaded by pf before the last step's loads and butterflies,
+    // so the table latency hides behind them; one multiply per element instead of two
+    constexpr int PERL = 16 / RR;
+    u64 tq[PERL][RR];
+    const u64* tab = a.t4 ? a.t4 + (INV ? 0 : ((u64)t << a.logn)) + col0 : nullptr;
+    auto pf = [&](int q, int seq, int base, int stride) {
+        if (!tab) return;
+#pragma unroll
+        for (int r = 0; r < RR; r++) tq[q][r] = tab[((u64)(base + r * stride) << a.logC) + seq];
+    };
+    auto stg = [&](int q, int seq, int base, int stride, u64* v) {
         const u64 j2 = col0 + seq;
+        if (tab) {
+#pragma unroll
+            for (int r = 0; r < RR; r++) y[((u64)(base + r * stride) << a.logC) + j2] = gl_mul(v[r], tq[q][r]);
+            return;
+        }
         u64 w, step;
         if (INV) {
             w = tw_get(a.T, a.logn, (j2 * (u64)base) & (n - 1), true);
@@ -240,7 +262,7 @@ __global__ __launch_bounds__(THREADS) void ntt_pass_a(NttArgs a) {
             if (r + 1 < RR) w = gl_mul(w, step);
         }
     };
-    pass_dft<LOGR, INV, true>(tile, logTC, ltw, ldg, stg);
+    pass_dft<LOGR, INV, true>(tile, logTC, ltw, ldg, stg, pf);
 }
 
 // ---------------------------------------------------------------- pass B: row DFTs (size C)
@@ -258,13 +280,13 @@ __global__ __launch_bounds__(THREADS) void ntt_pass_b(NttArgs a) {
     __syncthreads();
     const u64* y = a.y + (u64)pt * n;
     auto ldg = [&](int seq, int j2) -> u64 { return y[((u64)(k10 + seq) << LOGC) + j2]; };
-    auto stg = [&](int seq, int base, int stride, u64* v) {
+    auto stg = [&](int, int seq, int base, int stride, u64* v) {
 #pragma unroll
         for (int r = 0; r < RR; r++) {
             const u64 k = (u64)(k10 + seq) + ((u64)(base + r * stride) << a.logR);
             if (INV) {
                 if (k < a.keep) {
-                    u64 x = gl_mul(v[r], a.scale);
+                    u64 x = a.t4 ? v[r] : gl_mul(v[r], a.scale);  // the table carries 1/n
                     if (a.off7) x = gl_mul(x, a.T.ipow7[k]);
                     a.out[(u64)pt * a.out_stride + k] = x;
                 }
@@ -275,7 +297,7 @@ __global__ __launch_bounds__(THREADS) void ntt_pass_b(NttArgs a) {
     };
     // multi-step rows: first step along the row (coalesced loads); one-step rows: lanes along
     // sequences so the (final) global store is coalesced
-    pass_dft<LOGC, INV, (Plan<LOGC>::NSTEP == 1)>(tile, logTR, ltw, ldg, stg);
+    pass_dft<LOGC, INV, (Plan<LOGC>::NSTEP == 1)>(tile, logTR, ltw, ldg, stg, [](int, int, int, int) {});
 }
 
 // ---------------------------------------------------------------- dispatch
@@ -311,23 +333,48 @@ static void run_pass_b(int logC, dim3 g, size_t lds, hipStream_t s, const NttArg
 #undef XFG_CASE_B
 }
 
-static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
-    // split n = R * C: evenly below 2^18, C = 2R from 2^18 on (faster at 2^18 and 2^20, see
-    // scripts/ntt_split.py); XFG_NTT_LOGC forces log2(C) for tuning sweeps
+// split n = R * C: evenly below 2^18, C = 2R from 2^18 on (faster at 2^18 and 2^20, see
+// scripts/ntt_split.py); XFG_NTT_LOGC forces log2(C) for tuning sweeps
+static void ntt_split(int logn, int& logR, int& logC) {
     static const int force_logc = [] {
         const char* v = getenv("XFG_NTT_LOGC");
         return v && *v ? atoi(v) : 0;
     }();
-    if (force_logc > 1 && force_logc <= 12 && a.logn - force_logc >= 1 && a.logn - force_logc <= 10) {
-        a.logC = force_logc;
-        a.logR = a.logn - a.logC;
-    } else if (a.logn >= 18) {  // measured (scripts/ntt_split.py): C one step wider than R at 2^18 / 2^20
-        a.logC = a.logn / 2 + 1;
-        a.logR = a.logn - a.logC;
+    if (force_logc > 1 && force_logc <= 12 && logn - force_logc >= 1 && logn - force_logc <= 10) {
+        logC = force_logc;
+    } else if (logn >= 18) {
+        logC = logn / 2 + 1;
     } else {
-        a.logR = a.logn / 2;
-        a.logC = a.logn - a.logR;
+        logC = logn - logn / 2;
     }
+    logR = logn - logC;
+}
+
+__global__ void fourstep_kernel(u64* out, int logn, int logbeta, int logC, u64 scale, Tables T) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    const u64 n = 1ULL << logn;
+    if (logbeta < 0) {
+        if (i >= n) return;
+        const u64 k1 = i >> logC, j2 = i & ((1ULL << logC) - 1);
+        out[i] = gl_mul(tw_get(T, logn, (j2 * k1) & (n - 1), true), scale);
+    } else {
+        const int logN = logn + logbeta;
+        if (i >= (1ULL << logN)) return;
+        const u64 t = i >> logn, k1 = (i & (n - 1)) >> logC, j2 = i & ((1ULL << logC) - 1);
+        out[i] = gl_mul(T.pow7[j2], tw_get(T, logN, (j2 * (t + (k1 << logbeta))) & ((1ULL << logN) - 1), false));
+    }
+}
+u64 fourstep_size(int logn, int logbeta) { return 1ULL << (logn + (logbeta > 0 ? logbeta : 0)); }
+void build_fourstep(u64* out, int logn, int logbeta, const Tables& T, hipStream_t s) {
+    int logR, logC;
+    ntt_split(logn, logR, logC);
+    const u64 cnt = fourstep_size(logn, logbeta);
+    hipLaunchKernelGGL(fourstep_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, out, logn, logbeta, logC,
+                       gl_inv(1ULL << logn), T);
+}
+
+static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
+    ntt_split(a.logn, a.logR, a.logC);
     const int R = 1 << a.logR, C = 1 << a.logC;
     const int logTC = a.logC < 12 - a.logR ? a.logC : 12 - a.logR;
     const int logTR = a.logR < 12 - a.logC ? a.logR : 12 - a.logC;
@@ -370,6 +417,7 @@ void launch_lde(const u64* coef, u64 coef_stride, u64* out, u64* scratch, int np
         a.logn = logn;
         a.logbeta = logbeta;
         a.T = T;
+        a.t4 = (T.fs && logn <= FOURSTEP_MAX_LOG && logbeta <= 4) ? T.fs->fwd[logn][logbeta] : nullptr;
         ntt_run(a, std::min(chunk, npoly - p0), false, s);
     }
 }
@@ -388,6 +436,7 @@ void launch_interpolate(const u64* evals, u64 in_stride, u64* out, u64 out_strid
     a.keep = keep;
     a.T = T;
     a.scale = gl_inv(1ULL << logn);
+    a.t4 = (T.fs && logn <= FOURSTEP_MAX_LOG) ? T.fs->inv[logn] : nullptr;
     ntt_run(a, npoly, true, s);
 }
 

@@ -205,6 +205,8 @@ struct TablesHost {
     int LM = -1;
     DBuf<u64> tw, pow7, ipow7;
     std::map<int, DBuf<u64>> ce_div;  // constraint divisor tables per log2(trace length)
+    FourStep fs;                      // four-step twiddle tables (pointers into four_buf)
+    std::map<int, DBuf<u64>> four_buf;
 };
 
 // Data-independent constraint divisors on the CE domain x_i = 7 w_2n^i (i = 2m + par), laid out
@@ -356,7 +358,35 @@ static Tables tables_of(xfg_ctx* c) {
     T.LM = c->tables.LM;
     T.pow7 = c->tables.pow7.p;
     T.ipow7 = c->tables.ipow7.p;
+    T.fs = &c->tables.fs;
     return T;
+}
+// four-step twiddle tables of the NTT sizes one (n, beta) proof uses: the forward LDE and the
+// inverse NTTs of sizes 8 .. 2n (trace, composition, FRI remainder). Sizes whose table would exceed
+// 2^FOURSTEP_MAX_LOG entries keep the running-product twiddles. Returns false when one is missing.
+static bool fourstep_ready(xfg_ctx* c, int logn, int logbeta) {
+    const FourStep& f = c->tables.fs;
+    if (logn + logbeta <= FOURSTEP_MAX_LOG && !f.fwd[logn][logbeta]) return false;
+    for (int l = 3; l <= std::min(logn + 1, FOURSTEP_MAX_LOG); l++)
+        if (!f.inv[l]) return false;
+    return true;
+}
+// caller guarantees no kernel in flight reads the registry (fresh context or drained)
+static void ensure_fourstep(xfg_ctx* c, int logn, int logbeta) {
+    if (fourstep_ready(c, logn, logbeta)) return;
+    ensure_tables(c, std::max(logn + logbeta, logn + 1));
+    const Tables T = tables_of(c);
+    auto build = [&](int ln, int lb) {
+        DBuf<u64>& b = c->tables.four_buf[ln * 8 + lb + 1];
+        b.ensure(fourstep_size(ln, lb));
+        build_fourstep(b.p, ln, lb, T, 0);
+        return (const u64*)b.p;
+    };
+    FourStep& f = c->tables.fs;
+    if (logn + logbeta <= FOURSTEP_MAX_LOG && !f.fwd[logn][logbeta]) f.fwd[logn][logbeta] = build(logn, logbeta);
+    for (int l = 3; l <= std::min(logn + 1, FOURSTEP_MAX_LOG); l++)
+        if (!f.inv[l]) f.inv[l] = build(l, -1);
+    HIPCHK(hipStreamSynchronize(0));
 }
 
 // D2H of the root (heap index 1) of B trees laid out with a per-proof stride
@@ -1034,9 +1064,10 @@ static void drain(xfg_ctx* c) {
 
 static void bind_tables(xfg_ctx* c, Batch* b) {
     const int LM = (int)(ilog2(b->n) + ilog2(b->o.beta));
-    if (c->tables.LM < LM) {
+    if (c->tables.LM < LM || !fourstep_ready(c, (int)ilog2(b->n), (int)ilog2(b->o.beta))) {
         drain(c);
         ensure_tables(c, LM);
+        ensure_fourstep(c, (int)ilog2(b->n), (int)ilog2(b->o.beta));
     }
     b->T = tables_of(c);
     b->ce_div = ensure_ce_table(c, (int)ilog2(b->n));
@@ -1151,6 +1182,7 @@ void xfg_ctx_destroy(xfg_ctx* c) {
     c->tables.pow7.release();
     c->tables.ipow7.release();
     for (auto& kv : c->tables.ce_div) kv.second.release();
+    for (auto& kv : c->tables.four_buf) kv.second.release();
     delete c;
 }
 
@@ -1413,6 +1445,7 @@ int xfg_bench_lde(xfg_ctx* c, uint32_t count, uint64_t n, uint32_t blowup, uint3
         const int logn = (int)ilog2(n), logbeta = (int)ilog2(blowup);
         const u64 N = n * blowup;
         ensure_tables(c, logn + logbeta);
+        ensure_fourstep(c, logn, logbeta);
         Tables T = tables_of(c);
         L->coef.ensure((size_t)count * 7 * n);
         L->scratch.ensure((size_t)count * 7 * N);
@@ -1454,6 +1487,7 @@ int xfg_debug_lde(xfg_ctx* c, const uint64_t* coef, uint32_t npoly, uint64_t n, 
         const int logn = (int)ilog2(n), logbeta = (int)ilog2(blowup);
         const u64 N = n * blowup;
         ensure_tables(c, logn + logbeta);
+        ensure_fourstep(c, logn, logbeta);
         Tables T = tables_of(c);
         L->coef.ensure((size_t)npoly * n);
         L->scratch.ensure((size_t)npoly * N);
@@ -1481,6 +1515,7 @@ int xfg_debug_interpolate(xfg_ctx* c, const uint64_t* evals, uint32_t npoly, uin
         HIPCHK(hipSetDevice(c->device));
         const int logn = (int)ilog2(n);
         ensure_tables(c, std::max(logn, c->tables.LM));
+        if (logn >= 4) ensure_fourstep(c, logn - 1, 1);  // inverse tables up to size n
         Tables T = tables_of(c);
         L->trace.ensure((size_t)npoly * n);
         L->coef.ensure((size_t)npoly * n);
