@@ -11,7 +11,7 @@ timeout -k 10 400 python3 bench.py ${BENCH_ARGS:---steps 20 --warmup 3} > $OUT/b
 cat $OUT/bench.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o bench -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > $OUT/trace.log 2>&1 || { echo "rocprof trace failed"; tail -5 $OUT/trace.log; exit 1; }
 i=0
-for grp in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES"; do
+for grp in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES" VALUBusy OccupancyPercent; do
   i=$((i+1))
   timeout -k 10 180 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc$i -o pmc -- python3 scripts/lde_only.py 64 > $OUT/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; tail -5 $OUT/pmc$i.log; exit 1; }
 done

@@ -41,6 +41,10 @@ if PA in acc and PB in acc:
                       "fetch_bytes_x2": int(fetch), "write_bytes": int(write),
                       "valu_insts_pass_a": mean(acc[PA].get("SQ_INSTS_VALU", [])),
                       "valu_insts_pass_b": mean(acc[PB].get("SQ_INSTS_VALU", [])),
+                      "valu_busy_pct_pass_a": round(mean(acc[PA].get("VALUBusy", [])), 1),
+                      "valu_busy_pct_pass_b": round(mean(acc[PB].get("VALUBusy", [])), 1),
+                      "occupancy_pct_pass_a": round(mean(acc[PA].get("OccupancyPercent", [])), 1),
+                      "occupancy_pct_pass_b": round(mean(acc[PB].get("OccupancyPercent", [])), 1),
                       "algorithmic_bytes": 8 * 7 * (65536 + 8 * 65536) * 64}
 stats = rows("trace/**/*kernel_stats.csv")
 res["top_kernels"] = [{"name": r["Name"][:80], "calls": int(r["Calls"]), "total_ms": round(float(r["TotalDurationNs"]) / 1e6, 3),
