@@ -169,32 +169,6 @@ void launch_open_rows(const u64* lde, int nc, const u64* entries, u64 count, Dig
     XFG_CHECK_LAUNCH();
 }
 
-// one thread per node of level `count >> H`: merges its 2^H descendants at level `count`
-// (heap [count, 2 count)) in registers and writes the H levels above them
-template <int H>
-__device__ __forceinline__ Digest up_subtree(const Digest* src, Digest* nodes, u64 first, int lvl_from_top) {
-    (void)lvl_from_top;
-    if constexpr (H == 0) {
-        return src[0];
-    } else {
-        Digest l = up_subtree<H - 1>(src, nodes, first, 0);
-        Digest r = up_subtree<H - 1>(src + (1 << (H - 1)), nodes, first + (1ULL << (H - 1)), 0);
-        Digest p = b3_merge(l, r);
-        nodes[first >> H] = p;
-        return p;
-    }
-}
-template <int H>
-__global__ __launch_bounds__(256) void tree_up_kernel(Digest* nodes_all, u64 node_stride, u64 count) {
-    const u64 idx = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (count >> H)) return;
-    Digest* nodes = nodes_all + (u64)blockIdx.y * node_stride;
-    const u64 first = count + (idx << H);
-    Digest ch[1 << H];
-#pragma unroll
-    for (int k = 0; k < (1 << H); k++) ch[k] = nodes[first + k];
-    up_subtree<H>(ch, nodes, first, 0);
-}
 // last levels (count <= 512): one block per tree, LDS
 __global__ __launch_bounds__(256) void tree_top_kernel(Digest* nodes_all, u64 node_stride, u64 count) {
     __shared__ Digest lds[256];
@@ -215,18 +189,22 @@ __global__ __launch_bounds__(256) void tree_top_kernel(Digest* nodes_all, u64 no
         __syncthreads();
     }
 }
+// middle levels: a block merges 512 consecutive nodes of level `count` (two per thread, coalesced)
+// and continues through LDS down to one node, writing every parent: count / 512 nodes remain
+__global__ __launch_bounds__(256) void tree_mid_kernel(Digest* nodes_all, u64 node_stride, u64 count) {
+    __shared__ Digest lds[256];
+    Digest* nodes = nodes_all + (u64)blockIdx.y * node_stride;
+    const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
+    const Digest d = b3_merge(nodes[count + 2 * i], nodes[count + 2 * i + 1]);
+    nodes[count / 2 + i] = d;
+    block_tree_up(d, nodes, count / 2, lds, 1);
+}
 void launch_tree_top(Digest* nodes, u64 node_stride, u64 count, int npoly, hipStream_t s) {
+    // one launch per 9 levels instead of one per level
     while (count > 512) {
-        int lg = 0;
-        while ((1ULL << (lg + 1)) <= count) lg++;
-        int h = 1;  // one coalesced merge per thread per level (multi-level variants gather 2^h
-                    // digests per lane uncoalesced and measured slower)
-        u64 outc = count >> h;
-        dim3 g((unsigned)((outc + 255) / 256), npoly);
-        if (h == 3) hipLaunchKernelGGL(tree_up_kernel<3>, g, dim3(256), 0, s, nodes, node_stride, count);
-        else if (h == 2) hipLaunchKernelGGL(tree_up_kernel<2>, g, dim3(256), 0, s, nodes, node_stride, count);
-        else hipLaunchKernelGGL(tree_up_kernel<1>, g, dim3(256), 0, s, nodes, node_stride, count);
-        count = outc;
+        hipLaunchKernelGGL(tree_mid_kernel, dim3((unsigned)(count / 512), npoly), dim3(256), 0, s, nodes, node_stride,
+                           count);
+        count /= 512;
     }
     if (count > 1) {
         int threads = (int)(count / 2);
