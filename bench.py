@@ -153,6 +153,14 @@ def config5(prover, batch=4, calls=5):
             "trace_lde_GBps": round(8 * WIDTH * (n5 + 16 * n5) / (lde_ms * 1e-3) / 1e9, 1)}
 
 
+def in_pipeline(ms, sets, polys, n):
+    if not sets:
+        return None
+    b = 8 * (n + n * BLOWUP) * polys
+    return {"launch_sets": sets, "avg_ms": round(ms / sets, 4), "polys_per_set": polys // sets,
+            "achieved_GBps": round(b / (ms * 1e-3) / 1e9, 1)}
+
+
 def pmc_traffic(per, n, blowup):
     """HBM bytes per trace-LDE launch set from the committed PMC pass (profiles/rNN/lde_pmc.json,
     made by scripts/profile_round.sh: FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 --pmc runs)"""
@@ -243,6 +251,7 @@ def main():
         pipelined_steps(submit_fn, collect_fn, batches[:args.warmup], rank, world, per, device, dist,
                         packed[:args.warmup] if packed else None)
     barrier()
+    prover.lde_probe(True)  # HIP events around every trace-LDE launch set inside the timed steps
     t0 = time.perf_counter()
     out = pipelined_steps(submit_fn, collect_fn, batches[args.warmup:], rank, world, per, device, dist,
                           packed[args.warmup:] if packed else None)
@@ -254,6 +263,7 @@ def main():
     el = float(el_t.item())
     if rank == 0:
         assert out is not None and len(out) == per * world
+    pipe_ms, pipe_sets, pipe_polys = prover.lde_probe(False)
 
     # one synchronous batch call (no pipelining), for reference
     t = time.perf_counter()
@@ -300,7 +310,10 @@ def main():
                          "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
                          "traffic_source": traffic_src,
                          "kernel": "trace LDE (ntt_pass_a<8,false> + ntt_pass_b<8,false>), 7 columns x "
-                                   f"{per} proofs, {lde_ms:.3f} ms/launch-set, {lde_bytes} algorithmic B"},
+                                   f"{per} proofs, {lde_ms:.3f} ms/launch-set, {lde_bytes} algorithmic B",
+                         # the same launch sets inside the timed pipelined steps (per 16-proof unit,
+                         # sharing the GPU with the other lanes' kernels)
+                         "in_pipeline": in_pipeline(pipe_ms, pipe_sets, pipe_polys, n)},
             "stage_ms_one_batch": prover_stage,
             "sync_prove_batch_ms": round(sync_call_ms, 3),
         }

@@ -170,6 +170,10 @@ int xfg_stage_times(const xfg_ctx* ctx, double* ms, const char** names, int max)
 /* times `iters` launches of the trace LDE kernels (7 columns x count proofs, resident device
  * buffers, HIP events on the context stream); returns average ms per launch set in *avg_ms */
 int xfg_bench_lde(xfg_ctx* ctx, uint32_t count, uint64_t n, uint32_t blowup, uint32_t iters, double* avg_ms);
+/* in-pipeline trace-LDE timing: HIP events around the trace LDE launch set of every proof unit
+ * (on the lane stream that launches it). enabled = 1 resets and starts; enabled = 0 stops. The
+ * totals so far (sum of launch-set durations, launch sets, polynomials) are returned either way. */
+int xfg_lde_probe(xfg_ctx* ctx, int enabled, double* total_ms, uint64_t* launch_sets, uint64_t* polys);
 /* kernel-level parity hooks (host buffers in/out) */
 int xfg_debug_lde(xfg_ctx* ctx, const uint64_t* coef, uint32_t npoly, uint64_t n, uint32_t blowup, uint64_t* out);
 int xfg_debug_interpolate(xfg_ctx* ctx, const uint64_t* evals, uint32_t npoly, uint64_t n, int offset7,

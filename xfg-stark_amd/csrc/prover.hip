@@ -253,6 +253,11 @@ struct Lane {
     bool timing = false;
     double stage_ms[ST_COUNT] = {0};
     hipEvent_t ev[ST_COUNT + 1] = {};
+    // xfg_lde_probe: events around the trace LDE launch set, totals of the units so far
+    bool lde_probe = false;
+    hipEvent_t lde_ev[2] = {};
+    double lde_ms = 0;
+    u64 lde_sets = 0, lde_polys = 0;
     DBuf<AirConst> air;
     DBuf<u64> coeffs, trace, coef, scratch, lde, ce, hcoef, hlde, zpts, partial, ood, carry, deep, f0, alpha7,
         rem, gidx, gval, dn2;
@@ -296,6 +301,7 @@ struct xfg_ctx {
     int device = 0;
     std::string err;
     bool timing = false;
+    bool lde_probe = false;  // xfg_lde_probe state, inherited by lanes created later
     xfg::TablesHost tables;
     std::vector<std::unique_ptr<xfg::Lane>> lanes;
     // persistent lane workers: one host thread per lane pulls proof units from a FIFO shared by
@@ -538,7 +544,16 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     if (trace_host) HIPCHK(hipMemcpyAsync(c->trace.p, trace_host, (size_t)B * 7 * n * 8, hipMemcpyHostToDevice, s));
     else launch_trace_gen(c->air.p, c->trace.p, logn, B, s);
     launch_interpolate(c->trace.p, n, c->coef.p, n, c->scratch.p, B * 7, logn, false, n, T, s);
+    const bool probe = c->lde_probe;
+    if (probe) {
+        if (!c->lde_ev[0]) {
+            HIPCHK(hipEventCreate(&c->lde_ev[0]));
+            HIPCHK(hipEventCreate(&c->lde_ev[1]));
+        }
+        HIPCHK(hipEventRecord(c->lde_ev[0], s));
+    }
     launch_lde(c->coef.p, n, c->lde.p, c->scratch.p, B * 7, logn, logbeta, T, s);
+    if (probe) HIPCHK(hipEventRecord(c->lde_ev[1], s));
     stage_mark(c, 1);
     launch_tree_top(c->tnodes.p, 2 * n, launch_leaves_lde(c->lde.p, 7, c->tnodes.p, 2 * n, B, logn, logbeta, s), B,
                     s);
@@ -915,6 +930,14 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     }
     ht.mark("serialize");
     ht.dump(B);
+    if (probe) {  // the stream has passed both events (root / query fetches synchronised it)
+        float ms = 0;
+        HIPCHK(hipEventSynchronize(c->lde_ev[1]));
+        HIPCHK(hipEventElapsedTime(&ms, c->lde_ev[0], c->lde_ev[1]));
+        c->lde_ms += ms;
+        c->lde_sets++;
+        c->lde_polys += (u64)B * 7;
+    }
     if (c->timing) {
         for (int k = 0; k < 9; k++) {
             float ms = 0;
@@ -931,6 +954,7 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
 static Lane* lane0(xfg_ctx* c) {
     if (c->lanes.empty()) {
         c->lanes.emplace_back(new Lane());
+        c->lanes[0]->lde_probe = c->lde_probe;
         HIPCHK(hipStreamCreateWithFlags(&c->lanes[0]->stream, hipStreamNonBlocking));
         for (auto& e : c->lanes[0]->ev) HIPCHK(hipEventCreate(&e));
     }
@@ -940,6 +964,7 @@ static void ensure_lanes(xfg_ctx* c, size_t k) {
     lane0(c);
     while (c->lanes.size() < k) {
         c->lanes.emplace_back(new Lane());
+        c->lanes.back()->lde_probe = c->lde_probe;
         HIPCHK(hipStreamCreateWithFlags(&c->lanes.back()->stream, hipStreamNonBlocking));
         for (auto& e : c->lanes.back()->ev) HIPCHK(hipEventCreate(&e));
     }
@@ -1176,6 +1201,8 @@ void xfg_ctx_destroy(xfg_ctx* c) {
         (void)hipStreamSynchronize(L->stream);
         L->release();
         for (auto& e : L->ev) (void)hipEventDestroy(e);
+        for (auto& e : L->lde_ev)
+            if (e) (void)hipEventDestroy(e);
         (void)hipStreamDestroy(L->stream);
     }
     c->tables.tw.release();
@@ -1472,6 +1499,28 @@ int xfg_bench_lde(xfg_ctx* c, uint32_t count, uint64_t n, uint32_t blowup, uint3
         *avg_ms = ms / iters;
         return XFG_OK;
     });
+}
+
+int xfg_lde_probe(xfg_ctx* c, int enabled, double* total_ms, uint64_t* launch_sets, uint64_t* polys) {
+    if (!c) return XFG_INVALID_ARGUMENT;
+    if (busy(c)) {  // lane counters belong to the workers while batches are pending
+        c->err = "batches pending: call xfg_batch_wait first";
+        return XFG_INVALID_ARGUMENT;
+    }
+    double ms = 0;
+    u64 sets = 0, np = 0;
+    for (auto& L : c->lanes) {
+        ms += L->lde_ms;
+        sets += L->lde_sets;
+        np += L->lde_polys;
+        if (enabled) L->lde_ms = 0, L->lde_sets = 0, L->lde_polys = 0;
+        L->lde_probe = enabled != 0;
+    }
+    if (total_ms) *total_ms = ms;
+    c->lde_probe = enabled != 0;
+    if (launch_sets) *launch_sets = sets;
+    if (polys) *polys = np;
+    return XFG_OK;
 }
 
 int xfg_debug_lde(xfg_ctx* c, const uint64_t* coef, uint32_t npoly, uint64_t n, uint32_t blowup, uint64_t* out) {

@@ -80,6 +80,8 @@ _lib.xfg_burn_air_consts.argtypes = [C.POINTER(_BurnInputs), C.POINTER(_AirConst
 _lib.xfg_set_timing.argtypes = [C.c_void_p, C.c_int]
 _lib.xfg_stage_times.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_char_p), C.c_int]
 _lib.xfg_bench_lde.argtypes = [C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.POINTER(C.c_double)]
+_lib.xfg_lde_probe.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_uint64),
+                               C.POINTER(C.c_uint64)]
 _lib.xfg_debug_lde.argtypes = [C.c_void_p, _u64p, C.c_uint32, C.c_uint64, C.c_uint32, _u64p]
 _lib.xfg_debug_ood_deep.argtypes = [C.c_void_p, C.c_uint32, C.c_uint64, _u64p, _u64p, _u64p, _u64p, _u64p, _u64p]
 _lib.xfg_debug_interpolate.argtypes = [C.c_void_p, _u64p, C.c_uint32, C.c_uint64, C.c_int, _u64p]
@@ -485,6 +487,15 @@ class XfgBurnMintProver:
         if st:
             raise self._err(st)
         return avg.value
+
+    def lde_probe(self, enabled):
+        """(total ms, launch sets, polynomials) of the trace-LDE launch sets timed in the proving
+        pipeline since the last lde_probe(True) (HIP events on the launching lane's stream)"""
+        ms, sets, polys = C.c_double(), C.c_uint64(), C.c_uint64()
+        st = _lib.xfg_lde_probe(self._ctx, 1 if enabled else 0, C.byref(ms), C.byref(sets), C.byref(polys))
+        if st:
+            raise self._err(st)
+        return ms.value, sets.value, polys.value
 
     def debug_lde(self, coef, n, blowup):
         import numpy as np
