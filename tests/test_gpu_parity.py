@@ -66,6 +66,28 @@ def test_interpolate_kernel_matches_oracle(prover, n, off7):
         assert [int(v) for v in got[p]] == want
 
 
+EDGE = [0, 1, 2, P - 1, P - 2, 0xFFFFFFFF, 0x100000000, 0xFFFFFFFF00000000, 1 << 63, (1 << 63) - 1, P - 0xFFFFFFFF]
+
+
+@pytest.mark.parametrize("n,blowup", [(4096, 8), (1 << 16, 8)])
+def test_ntt_edge_values_match_oracle(prover, n, blowup):
+    """boundary field values (all p - 1, all 0 but one, alternating extremes, random picks from
+    EDGE): the weakly reduced butterflies and the carry-based reductions must agree with the
+    oracle's canonical arithmetic"""
+    rng = np.random.default_rng(7)
+    polys = np.stack([np.full(n, P - 1, dtype=np.uint64),
+                      np.array([EDGE[i % len(EDGE)] for i in range(n)], dtype=np.uint64),
+                      np.array(rng.choice(EDGE, size=n), dtype=np.uint64),
+                      np.where(np.arange(n) % 2 == 0, np.uint64(P - 1), np.uint64(0xFFFFFFFF00000000))])
+    got = prover.debug_lde(polys, n, blowup)
+    for p in range(len(polys)):
+        assert [int(v) for v in got[p]] == O.evaluate_lde([int(v) for v in polys[p]], blowup, 7), p
+    for off7 in (False, True):
+        got = prover.debug_interpolate(polys, n, off7)
+        for p in range(len(polys)):
+            assert [int(v) for v in got[p]] == O.interpolate([int(v) for v in polys[p]], 7 if off7 else 1), (p, off7)
+
+
 def _ood_deep_reference(co, h, z, zg, a, gam):
     """T_c(z), T_c(zg), H(z) and the DEEP quotient coefficients (synthetic division), plain ints"""
     n = len(h)

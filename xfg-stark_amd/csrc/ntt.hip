@@ -46,7 +46,21 @@ __host__ __device__ constexpr int brev_c(int x, int bits) {
     return r;
 }
 
-// in-register DFT of size 2^LOGR (<= 16): v[q] <- sum_r v[r] w_R^(+-rq), natural order in/out
+// Weakly reduced values: any u64 congruent mod p. The butterflies keep their outputs weak and
+// reduce only the subtrahend / addend t (which must be < p for these forms): u + t carries at most
+// once past 2^64 when t < p, and u - t borrows into a value >= EPS when t < p.
+__device__ __forceinline__ u64 add_w(u64 a, u64 b) {  // b < p
+    u64 s;
+    const bool c = __builtin_add_overflow(a, b, &s);
+    return s + (c ? EPS : 0);
+}
+__device__ __forceinline__ u64 sub_w(u64 a, u64 b) { return add_w(a, P - b); }  // b < p
+__device__ __forceinline__ u64 canon(u64 x) { return x >= P ? x - P : x; }
+
+// in-register DFT of size 2^LOGR (<= 16): v[q] <- sum_r v[r] w_R^(+-rq), natural order in/out.
+// In: v[r] < p for every r whose bit-reversed position is odd (the level-0 subtrahends: every
+// r >= R/2), the rest may be weak. Out: weak. The shift multiplies return canonical values, so
+// only the w = 1 subtrahends of levels >= 1 are reduced explicitly.
 template <int LOGR, bool INV>
 __device__ __forceinline__ void dft_reg(u64* v) {
     constexpr int R = 1 << LOGR;
@@ -62,13 +76,14 @@ __device__ __forceinline__ void dft_reg(u64* v) {
             int e = (root_exp2(s + 1) * pos) % 192;
             if (INV && e) e = 192 - e;
             // w = 2^e = -2^(e - 96) for e >= 96: the sign swaps the butterfly's add and sub
-            const u64 t = mul_pow2(a[i0 + h], e % 96), u = a[i0];
+            const u64 x = a[i0 + h];
+            const u64 t = (e % 96) ? mul_pow2(x, e % 96) : (s == 0 ? x : canon(x)), u = a[i0];
             if (e >= 96) {
-                a[i0] = gl_sub(u, t);
-                a[i0 + h] = gl_add(u, t);
+                a[i0] = sub_w(u, t);
+                a[i0 + h] = add_w(u, t);
             } else {
-                a[i0] = gl_add(u, t);
-                a[i0 + h] = gl_sub(u, t);
+                a[i0] = add_w(u, t);
+                a[i0 + h] = sub_w(u, t);
             }
         }
     }
@@ -203,7 +218,7 @@ struct NttArgs {
 //   y[t][k1][j2] = X[k1] * 7^j2 * w_N^(j2 (t + beta k1))
 // inverse: y[k1][j2] = X[k1] * w_n^-(j2 k1)
 template <int LOGR, bool INV>
-__global__ __launch_bounds__(THREADS) void ntt_pass_a(NttArgs a) {
+__global__ __launch_bounds__(THREADS, 4) void ntt_pass_a(NttArgs a) {
     constexpr int R = 1 << LOGR, PITCH = row_pitch(R), RR = Plan<LOGR>::LAST_R;
     extern __shared__ u64 lds[];
     const int logTC = (a.logC < 12 - LOGR) ? a.logC : 12 - LOGR;
@@ -286,12 +301,12 @@ __global__ __launch_bounds__(THREADS) void ntt_pass_b(NttArgs a) {
             const u64 k = (u64)(k10 + seq) + ((u64)(base + r * stride) << a.logR);
             if (INV) {
                 if (k < a.keep) {
-                    u64 x = a.t4 ? v[r] : gl_mul(v[r], a.scale);  // the table carries 1/n
+                    u64 x = a.t4 ? canon(v[r]) : gl_mul(v[r], a.scale);  // the table carries 1/n
                     if (a.off7) x = gl_mul(x, a.T.ipow7[k]);
                     a.out[(u64)pt * a.out_stride + k] = x;
                 }
             } else {
-                a.out[(u64)pt * n + k] = v[r];  // pt = poly * beta + t -> coset-major
+                a.out[(u64)pt * n + k] = canon(v[r]);  // pt = poly * beta + t -> coset-major
             }
         }
     };
