@@ -18,3 +18,7 @@ for name, fn in (("host", lambda: v.batch_verify(items, threads=16)), ("gpu", la
         fn()
     dt = (time.perf_counter() - t) / 3
     print(f"{name}: {k} proofs in {dt*1e3:.1f} ms -> {k/dt:.0f} proofs/s")
+if os.environ.get("XFG_TRACE") == "1":  # Python-side share of one GPU call
+    import cProfile, pstats
+    cProfile.run("v.batch_verify(items, gpu=pr)", "/tmp/vb.prof")
+    pstats.Stats("/tmp/vb.prof").sort_stats("cumulative").print_stats(12)

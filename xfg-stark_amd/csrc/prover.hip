@@ -320,6 +320,8 @@ struct xfg_ctx {
         xfg::DBuf<uint8_t> dstage;
         xfg::DBuf<uint32_t> flags;
         xfg::DBuf<xfg::Digest> dig, rootdig;
+        std::vector<xfg::VState> st;        // per-proof transcript states, reused between calls
+        std::vector<xfg::VerifyPlan> frag;  // per-proof plan fragments, reused between calls
     } vb;
 };
 
@@ -1645,7 +1647,12 @@ int xfg_verify_batch_gpu(xfg_ctx* c, uint32_t count, const uint8_t* const* proof
         const Opts acc = to_opts(acceptable);
         HostTrace ht;
         ht.mark("start");
-        std::vector<VState> st(count);
+        // per-proof transcript states and plan fragments are kept in the context between calls
+        // (reset in place: a large batch would otherwise allocate and free ~10^5 small blocks)
+        auto& V = c->vb;
+        if (V.st.size() < count) V.st.resize(count);
+        if (V.frag.size() < count) V.frag.resize(count);
+        std::vector<VState>& st = V.st;
         std::vector<std::string> err(count);
         const unsigned nt = std::max(1u, std::min<unsigned>(std::thread::hardware_concurrency(), 16));
         auto parallel = [&](const std::function<void(uint32_t)>& f) {
@@ -1673,8 +1680,9 @@ int xfg_verify_batch_gpu(xfg_ctx* c, uint32_t count, const uint8_t* const* proof
         //    prefix sum of the accepted proofs' lengths
         std::vector<size_t> boff(count + 1, 0);
         for (uint32_t i = 0; i < count; i++) boff[i + 1] = boff[i] + (err[i].empty() ? lens[i] : 0);
-        std::vector<VerifyPlan> frag(count);
+        std::vector<VerifyPlan>& frag = V.frag;
         parallel([&](uint32_t i) {
+            reset_plan(frag[i]);
             if (!err[i].empty()) return;
             std::string e;
             if (!plan_proof(st[i], boff[i], frag[i], e)) err[i] = e;
@@ -1687,7 +1695,8 @@ int xfg_verify_batch_gpu(xfg_ctx* c, uint32_t count, const uint8_t* const* proof
         };
         std::vector<Off> fo(count + 1);
         size_t nrounds = 0;
-        for (uint32_t i = 0; i < count; i++) nrounds = std::max(nrounds, frag[i].rounds.size());
+        for (uint32_t i = 0; i < count; i++)
+            if (err[i].empty()) nrounds = std::max(nrounds, frag[i].rounds.size());
         std::vector<std::vector<size_t>> rcount(nrounds, std::vector<size_t>(count + 1, 0));
         std::vector<int> planned(count, -1);
         int nplanned = 0;
@@ -1713,7 +1722,6 @@ int xfg_verify_batch_gpu(xfg_ctx* c, uint32_t count, const uint8_t* const* proof
                      o_r = al(o_lv + fo[count].lv * sizeof(VLeaf)), o_fp = al(o_r + rbase[nrounds] * 4),
                      o_fq = al(o_fp + fo[count].fp * sizeof(VFieldProof)),
                      o_ri = al(o_fq + fo[count].q * sizeof(VFieldQuery)), total_b = al(o_ri + fo[count].root * 8);
-        auto& V = c->vb;
         uint8_t* H = V.stage.ensure(total_b);
         VGather* hg = (VGather*)(H + o_g);
         VLeaf* hl = (VLeaf*)(H + o_lv);

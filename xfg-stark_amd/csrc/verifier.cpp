@@ -123,9 +123,13 @@ std::string parse_proof(const uint8_t* bytes, size_t len, ParsedProof& pf) {
 // BatchMerkleProof::get_root: the node vectors must hold exactly the siblings the opening plan of
 // `idx` asks for; every node on the way to the root is then recomputed, level by level.
 bool merkle_symbolic(const std::vector<u64>& idx, const Paths& paths, u64 L, MerkleSym& out) {
-    BatchOpening plan;
+    thread_local BatchOpening plan;
     plan_batch_opening(idx, L, plan);
-    out = MerkleSym();
+    // reset in place: callers reuse `out`, so steady-state planning does not allocate
+    out.nslots = out.root = 0;
+    out.leaf_slot.clear();
+    out.given.clear();
+    for (auto& v : out.levels) v.clear();
     if (plan.size() != paths.ptr.size()) return false;
     const unsigned depth = ilog2(L);
     // nodes available per level (0 = leaves) as (heap index, slot), sorted before use; per-thread
@@ -152,7 +156,8 @@ bool merkle_symbolic(const std::vector<u64>& idx, const Paths& paths, u64 L, Mer
     for (size_t i = 0; i < idx.size(); i++) level[i] = L + idx[i];
     std::sort(level.begin(), level.end());
     level.erase(std::unique(level.begin(), level.end()), level.end());
-    out.levels.resize(depth);
+    if (out.levels.size() < depth) out.levels.resize(depth);
+    out.nlev = depth;
     for (unsigned l = 0; l < depth; l++) {
         auto& cur = lv[l];
         std::sort(cur.begin(), cur.end());
@@ -192,8 +197,10 @@ static bool batch_root(const std::vector<u64>& idx, const std::vector<Digest>& l
     std::vector<Digest> val(sym.nslots);
     for (size_t i = 0; i < idx.size(); i++) val[sym.leaf_slot[i]] = leaf[i];
     for (auto& g : sym.given) memcpy(val[g.first].w, g.second, 32);
-    for (auto& lvl : sym.levels)
+    for (unsigned l = 0; l < sym.nlev; l++) {
+        const auto& lvl = sym.levels[l];
         for (size_t t = 0; t < lvl.size(); t += 3) val[lvl[t]] = b3_merge(val[lvl[t + 1]], val[lvl[t + 2]]);
+    }
     root = val[sym.root];
     return true;
 }
@@ -444,6 +451,17 @@ static std::string verify_proof(const uint8_t* bytes, size_t len, const AirConst
 }
 
 // ------------------------------------------------------------------ batched GPU verification plan
+void reset_plan(VerifyPlan& plan) {
+    plan.blob.clear();
+    plan.gathers.clear();
+    plan.leaves.clear();
+    for (auto& r : plan.rounds) r.clear();
+    plan.fproofs.clear();
+    plan.fqueries.clear();
+    plan.nslots = 0;
+    plan.roots.clear();
+    plan.fidx.clear();
+}
 bool plan_proof(const VState& st, size_t blob_off, VerifyPlan& plan, std::string& err) {
     const ParsedProof& pf = st.pf;
     const int de = st.de;
@@ -455,7 +473,8 @@ bool plan_proof(const VState& st, size_t blob_off, VerifyPlan& plan, std::string
     }
     auto off = [&](const uint8_t* p) { return (u64)blob_off + (u64)(p - pf.base); };
     // FRI position lists and the structural checks of the host verifier
-    std::vector<std::vector<u64>> fps(nl);
+    thread_local std::vector<std::vector<u64>> fps;
+    fps.resize(nl);
     {
         std::vector<u64> cur = st.pos;
         u64 D = N;
@@ -476,17 +495,18 @@ bool plan_proof(const VState& st, size_t blob_off, VerifyPlan& plan, std::string
         }
     }
     // Merkle trees: leaves, given nodes, merges by level -> digest slots
-    std::vector<int64_t> roots;
+    plan.roots.emplace_back();
+    std::vector<int64_t>& roots = plan.roots.back();
     auto add_tree = [&](const std::vector<u64>& idx, const Paths& paths, u64 L, const uint8_t* leaf0, size_t stride,
                         uint32_t words) -> int64_t {
-        MerkleSym sym;
+        thread_local MerkleSym sym;
         if (!merkle_symbolic(idx, paths, L, sym)) return -1;
         const uint32_t b = plan.nslots;
         for (size_t i = 0; i < idx.size(); i++)
             plan.leaves.push_back(VLeaf{off(leaf0 + i * stride), words, b + sym.leaf_slot[i]});
         for (auto& g : sym.given) plan.gathers.push_back(VGather{off(g.second), b + g.first, 0});
-        if (plan.rounds.size() < sym.levels.size()) plan.rounds.resize(sym.levels.size());
-        for (size_t r = 0; r < sym.levels.size(); r++)
+        if (plan.rounds.size() < sym.nlev) plan.rounds.resize(sym.nlev);
+        for (size_t r = 0; r < sym.nlev; r++)
             for (uint32_t x : sym.levels[r]) plan.rounds[r].push_back(b + x);
         plan.nslots += sym.nslots;
         return (int64_t)(b + sym.root);
@@ -501,7 +521,6 @@ bool plan_proof(const VState& st, size_t blob_off, VerifyPlan& plan, std::string
             D = rows;
         }
     }
-    plan.roots.push_back(roots);
     // field checks
     VFieldProof F{};
     F.z = st.z;

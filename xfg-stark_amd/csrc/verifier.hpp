@@ -67,6 +67,7 @@ struct MerkleSym {
     std::vector<uint32_t> leaf_slot;                         // per queried leaf
     std::vector<std::pair<uint32_t, const uint8_t*>> given;  // slot, digest bytes in the proof
     std::vector<std::vector<uint32_t>> levels;               // per level: out, left, right slots
+    unsigned nlev = 0;                                       // levels in use (levels may hold more)
 };
 bool merkle_symbolic(const std::vector<u64>& idx, const Paths& paths, u64 L, MerkleSym& out);
 
@@ -114,6 +115,8 @@ struct VerifyPlan {
 };
 // add one proof whose transcript replayed fine; false (+ err) on a structural error
 bool plan_proof(const VState& st, size_t blob_off, VerifyPlan& plan, std::string& err);
+// empty a plan for reuse, keeping its allocations
+void reset_plan(VerifyPlan& plan);
 // the host part after the device work: first failing check in the verifier's order, "" if none
 std::string finish_proof(const VState& st, const std::vector<Digest>& roots, uint32_t flags);
 
