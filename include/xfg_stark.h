@@ -178,6 +178,10 @@ int xfg_lde_probe(xfg_ctx* ctx, int enabled, double* total_ms, uint64_t* launch_
 int xfg_debug_lde(xfg_ctx* ctx, const uint64_t* coef, uint32_t npoly, uint64_t n, uint32_t blowup, uint64_t* out);
 int xfg_debug_interpolate(xfg_ctx* ctx, const uint64_t* evals, uint32_t npoly, uint64_t n, int offset7,
                           uint64_t* out);
+/* Goldilocks primitive self test on the device: out[i] = op(a[i], b[i]) with op 0 mul, 1 add,
+ * 2 sub, 3 canonical(a), 4 a * 2^(b mod 96), 5 a + (b mod 2^32) * (2^32 - 1), 6 a - b with one
+ * borrow fold (the weak subtraction of the NTT butterflies) */
+int xfg_debug_field(xfg_ctx* ctx, uint32_t op, uint64_t count, const uint64_t* a, const uint64_t* b, uint64_t* out);
 /* OOD evaluation + DEEP quotient kernels of the prover on `count` instances: coef [count][7][n],
  * hcoef [count][n] (trace / composition coefficients), zpts [count][2] = (z, z g), coeffs
  * [count][8] = 7 trace DEEP coefficients + the composition one; ood_out [count][15] (T_c(z),

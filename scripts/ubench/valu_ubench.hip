@@ -8,10 +8,10 @@
         unsigned a0 = threadIdx.x, a1 = a0 * 3, a2 = a0 * 5, a3 = a0 * 7, a4 = a0 + 1, a5 = a0 + 2, \
                  a6 = a0 + 3, a7 = a0 + 4, k = blockIdx.x | 1;                                  \
         for (int it = 0; it < iters; it++) {                                                     \
-            REP8(asm volatile(ASM : "+v"(a0) : "v"(k)); asm volatile(ASM : "+v"(a1) : "v"(k));   \
-                 asm volatile(ASM : "+v"(a2) : "v"(k)); asm volatile(ASM : "+v"(a3) : "v"(k));   \
-                 asm volatile(ASM : "+v"(a4) : "v"(k)); asm volatile(ASM : "+v"(a5) : "v"(k));   \
-                 asm volatile(ASM : "+v"(a6) : "v"(k)); asm volatile(ASM : "+v"(a7) : "v"(k));)  \
+            REP8(asm volatile(ASM : "+v"(a0) : "v"(k) : "vcc", "s40", "s41"); asm volatile(ASM : "+v"(a1) : "v"(k) : "vcc", "s40", "s41");   \
+                 asm volatile(ASM : "+v"(a2) : "v"(k) : "vcc", "s40", "s41"); asm volatile(ASM : "+v"(a3) : "v"(k) : "vcc", "s40", "s41");   \
+                 asm volatile(ASM : "+v"(a4) : "v"(k) : "vcc", "s40", "s41"); asm volatile(ASM : "+v"(a5) : "v"(k) : "vcc", "s40", "s41");   \
+                 asm volatile(ASM : "+v"(a6) : "v"(k) : "vcc", "s40", "s41"); asm volatile(ASM : "+v"(a7) : "v"(k) : "vcc", "s40", "s41");)  \
         }                                                                                        \
         out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;       \
     }
@@ -38,10 +38,10 @@ DEF(k_lshrrev, "v_lshrrev_b32_e32 %0, 7, %0")
                            a5 = a0 + 2, a6 = a0 + 3, a7 = a0 + 4, k = blockIdx.x | 1;           \
         unsigned k32 = blockIdx.x | 1;                                                            \
         for (int it = 0; it < iters; it++) {                                                     \
-            REP8(asm volatile(ASM : "+v"(a0) : "v"(k), "v"(k32) : "vcc"); asm volatile(ASM : "+v"(a1) : "v"(k), "v"(k32) : "vcc"); \
-                 asm volatile(ASM : "+v"(a2) : "v"(k), "v"(k32) : "vcc"); asm volatile(ASM : "+v"(a3) : "v"(k), "v"(k32) : "vcc"); \
-                 asm volatile(ASM : "+v"(a4) : "v"(k), "v"(k32) : "vcc"); asm volatile(ASM : "+v"(a5) : "v"(k), "v"(k32) : "vcc"); \
-                 asm volatile(ASM : "+v"(a6) : "v"(k), "v"(k32) : "vcc"); asm volatile(ASM : "+v"(a7) : "v"(k), "v"(k32) : "vcc");) \
+            REP8(asm volatile(ASM : "+v"(a0) : "v"(k), "v"(k32) : "vcc", "s40", "s41"); asm volatile(ASM : "+v"(a1) : "v"(k), "v"(k32) : "vcc", "s40", "s41"); \
+                 asm volatile(ASM : "+v"(a2) : "v"(k), "v"(k32) : "vcc", "s40", "s41"); asm volatile(ASM : "+v"(a3) : "v"(k), "v"(k32) : "vcc", "s40", "s41"); \
+                 asm volatile(ASM : "+v"(a4) : "v"(k), "v"(k32) : "vcc", "s40", "s41"); asm volatile(ASM : "+v"(a5) : "v"(k), "v"(k32) : "vcc", "s40", "s41"); \
+                 asm volatile(ASM : "+v"(a6) : "v"(k), "v"(k32) : "vcc", "s40", "s41"); asm volatile(ASM : "+v"(a7) : "v"(k), "v"(k32) : "vcc", "s40", "s41");) \
         }                                                                                        \
         out[blockIdx.x * blockDim.x + threadIdx.x] = (unsigned)(a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7); \
     }
@@ -54,6 +54,18 @@ DEF(k_subco, "v_sub_co_u32_e64 %0, vcc, %0, %1")
 DEF(k_subb, "v_subb_co_u32_e32 %0, vcc, %0, %1, vcc")
 DEF(k_cnd64, "v_cndmask_b32_e64 %0, %0, %1, vcc")
 DEF(k_mov, "v_mov_b32 %0, %1")
+DEF(k_addc, "v_addc_co_u32 %0, vcc, %0, %1, vcc")
+DEF(k_cmp32, "v_cmp_lt_u32_e32 vcc, %0, %1")
+DEF(k_sub, "v_sub_u32 %0, %0, %1")
+DEF(k_and, "v_and_b32 %0, %0, %1")
+DEF(k_mul24, "v_mul_u32_u24 %0, %0, %1")
+DEF(k_addco_s, "v_add_co_u32_e64 %0, s[40:41], %0, %1")
+DEF(k_addc_s, "v_addc_co_u32_e64 %0, s[40:41], %0, %1, s[40:41]")
+DEF(k_lshl_add32, "v_lshl_add_u32 %0, %0, 3, %1")
+DEF(k_cnd_s, "v_cndmask_b32_e64 %0, %0, %1, s[40:41]")
+DEF(k_bfe, "v_bfe_u32 %0, %0, 8, 16")
+DEF64(k_lshr64, "v_lshrrev_b64 %0, 7, %0")
+DEF64(k_mulhi64a, "v_mad_u64_u32 %0, s[40:41], %2, %2, %0")
 
 int main() {
     unsigned* d;
@@ -66,7 +78,11 @@ int main() {
         {"v_xor_b32_sdwa", k_sdwa_xor}, {"v_add_u32_sdwa", k_sdwa_add}, {"v_cndmask_b32", k_cndmask},
         {"v_lshrrev_b32", k_lshrrev}, {"v_lshl_add_u64", k_lshladd64}, {"v_cmp_lt_u64", k_cmp64},
         {"v_mad_u64_u32", k_mad64}, {"v_lshlrev_b64", k_lshl64}, {"v_mov_b64", k_mov64}, {"v_sub_co_u32_e64", k_subco},
-        {"v_subb_co_u32", k_subb}, {"v_cndmask_b32_e64", k_cnd64}, {"v_mov_b32", k_mov}};
+        {"v_subb_co_u32", k_subb}, {"v_cndmask_b32_e64", k_cnd64}, {"v_mov_b32", k_mov},
+        {"v_addc_co_u32", k_addc}, {"v_cmp_lt_u32", k_cmp32}, {"v_sub_u32", k_sub}, {"v_and_b32", k_and},
+        {"v_mul_u32_u24", k_mul24}, {"v_add_co_u32_e64 s", k_addco_s}, {"v_addc_co_u32_e64 s", k_addc_s},
+        {"v_lshl_add_u32", k_lshl_add32}, {"v_cndmask_e64 s", k_cnd_s}, {"v_bfe_u32", k_bfe},
+        {"v_lshrrev_b64", k_lshr64}, {"v_mad_u64_u32 s", k_mulhi64a}};
     for (auto& k : ks) {
         hipEvent_t a, b;
         hipEventCreate(&a);

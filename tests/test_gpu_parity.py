@@ -55,6 +55,55 @@ def test_lde_kernel_matches_oracle(prover, n, blowup):
         assert [int(v) for v in got[p]] == want
 
 
+P_GL = (1 << 64) - (1 << 32) + 1
+_EDGE = [0, 1, 2, 3, (1 << 32) - 1, 1 << 32, (1 << 32) + 1, (1 << 63) - 1, 1 << 63, P_GL - 2, P_GL - 1,
+         P_GL, P_GL + 1, (1 << 64) - 2, (1 << 64) - 1, 0xFFFFFFFF00000000, 0x00000000FFFFFFFE]
+
+
+def _field_inputs(canonical, seed):
+    rng = random.Random(seed)
+    vals = [v for v in _EDGE if not canonical or v < P_GL]
+    a = [x for x in vals for _ in vals] + [rng.randrange(P_GL if canonical else 1 << 64) for _ in range(20000)]
+    b = [y for _ in vals for y in vals] + [rng.randrange(P_GL if canonical else 1 << 64) for _ in range(20000)]
+    return a, b
+
+
+@pytest.mark.parametrize("op", ["mul", "add", "sub", "canon", "pow2", "fold", "sub_weak"])
+def test_field_primitives_match_bigint(prover, op):
+    """the gfx950 inline-asm Goldilocks primitives (gl.hpp) against Python integers, edge values
+    (0, 2^32 - 1, p - 1, p, 2^64 - 1, ...) crossed with each other plus random operands"""
+    canonical_in = op in ("add", "sub")
+    a, b = _field_inputs(canonical_in, hash(op) & 0xFFFF)
+    if op == "pow2":
+        b = [y % 96 for y in b]
+    if op == "fold":
+        b = [y & 0xFFFFFFFF for y in b]
+    if op == "sub_weak":  # butterfly contract: subtrahend < p
+        b = [y % P_GL for y in b]
+    got = prover.debug_field(op, np.array(a, dtype=np.uint64), np.array(b, dtype=np.uint64)).tolist()
+    for x, y, r in zip(a, b, got):
+        if op == "mul":
+            want = x * y % P_GL
+        elif op == "add":
+            want = (x + y) % P_GL
+        elif op == "sub":
+            want = (x - y) % P_GL
+        elif op == "canon":
+            want = x % P_GL
+        elif op == "pow2":
+            want = x * pow(2, y, P_GL) % P_GL
+            if y == 0:  # identity: returned as is
+                assert r == x
+                continue
+        elif op == "fold":
+            want = (x + y * 0xFFFFFFFF) % P_GL
+        else:
+            want = x - y if x >= y else x - y + P_GL
+            assert r == want, (op, x, y, r, want)
+            continue
+        assert r == want, (op, x, y, r, want)
+
+
 @pytest.mark.parametrize("n,off7", [(8, False), (64, True), (2048, False), (2048, True), (1 << 14, True),
                                     (1 << 17, True), (1 << 20, False)])
 def test_interpolate_kernel_matches_oracle(prover, n, off7):

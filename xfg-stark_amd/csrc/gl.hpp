@@ -16,16 +16,25 @@ constexpr u64 EPS = 0xFFFFFFFFULL;  // 2^64 mod p
 constexpr u64 GEN = 7;              // multiplicative generator == Winterfell domain offset
 constexpr u64 TWO_ADIC_ROOT = 1753635133440165772ULL;  // 7^((p-1)/2^32)
 
+__device__ __forceinline__ u64 gl_add_dev(u64 a, u64 b);
+__device__ __forceinline__ u64 gl_sub_weak(u64 a, u64 b);
 __host__ __device__ __forceinline__ u64 gl_add(u64 a, u64 b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return gl_add_dev(a, b);
+#else
     // a + b == a - (p - b); the borrow case adds p back, i.e. subtracts EPS mod 2^64
-    // (measured on gfx950: 6.0 T/s vs 4.2 T/s for the carry + compare form)
     u64 q = P - b;
     u64 d = a - q;
     return (a < q) ? d - EPS : d;
+#endif
 }
 __host__ __device__ __forceinline__ u64 gl_sub(u64 a, u64 b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return gl_sub_weak(a, b);  // canonical for canonical a, b
+#else
     u64 d = a - b;
     return (a < b) ? d - EPS : d;  // borrowed: -2^64 == -EPS
+#endif
 }
 __host__ __device__ __forceinline__ u64 gl_neg(u64 a) { return a ? P - a : 0; }
 
@@ -53,17 +62,113 @@ __host__ __device__ __forceinline__ u64 gl_reduce(u64 hi, u64 lo) {
     t0 = b ? t0 - EPS : t0;  // borrowed: + p == - EPS (mod 2^64), cannot wrap since t0 >= 2^64 - 2^32
     return gl_add_small(t0, (hl << 32) - hl);
 }
+// ---- gfx950 instruction-level forms. The VALU is the bound of every kernel of this path, so these
+// are written for instruction count: v_mad_u64_u32's carry-out and 64-bit selects by a 0/1 multiple
+// of EPS replace the compiler's compare-and-select lowering. Every VALU write of an SGPR mask that a
+// VALU reads back inside a statement is followed by >= 2 wait states (s_nop 1), VALU -> SALU and
+// SALU -> VALU mask hand-offs need none (both as the compiler itself emits them).
+
+// canonical lo + h * EPS for any lo and h < 2^32 (4 VALU + 1 SALU): r = lo + h EPS (carry c1);
+// c1 or r >= p selects r + EPS mod 2^64 (= r + 2^64 mod p when c1, r - p otherwise)
+__device__ __forceinline__ u64 gl_fold(u64 lo, u32 h) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    u64 r, out, c1, c2;
+    u32 sel;
+    asm("v_mad_u64_u32 %[r], %[c1], %[h], -1, %[lo]\n\t"
+        "v_cmp_lt_u64_e64 %[c2], %[pm1], %[r]\n\t"
+        "s_or_b64 %[c1], %[c1], %[c2]\n\t"
+        "v_cndmask_b32_e64 %[sel], 0, 1, %[c1]\n\t"
+        "v_mad_u64_u32 %[out], %[c2], %[sel], -1, %[r]"
+        : [r] "=&v"(r), [out] "=&v"(out), [sel] "=&v"(sel), [c1] "=&s"(c1), [c2] "=&s"(c2)
+        : [h] "v"(h), [lo] "v"(lo), [pm1] "s"(P - 1)
+        : "scc");
+    return out;
+#else
+    u64 r = lo + (u64)h * EPS;
+    const bool c = r < lo;
+    return (c || r >= P) ? r + EPS : r;
+#endif
+}
+// canonical a + b for canonical a, b (5 VALU + 1 SALU): s = a + b (carry c1); c1 or s >= p selects
+// s + EPS mod 2^64
+__device__ __forceinline__ u64 gl_add_dev(u64 a, u64 b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    u64 s, out, c1, c2;
+    u32 sel;
+    asm("v_lshl_add_u64 %[s], %[a], 0, %[b]\n\t"
+        "v_cmp_lt_u64_e64 %[c1], %[s], %[b]\n\t"
+        "v_cmp_lt_u64_e64 %[c2], %[pm1], %[s]\n\t"
+        "s_or_b64 %[c1], %[c1], %[c2]\n\t"
+        "v_cndmask_b32_e64 %[sel], 0, 1, %[c1]\n\t"
+        "v_mad_u64_u32 %[out], %[c2], %[sel], -1, %[s]"
+        : [s] "=&v"(s), [out] "=&v"(out), [sel] "=&v"(sel), [c1] "=&s"(c1), [c2] "=&s"(c2)
+        : [a] "v"(a), [b] "v"(b), [pm1] "s"(P - 1)
+        : "scc");
+    return out;
+#else
+    u64 s = a + b;
+    return (s < b || s >= P) ? s + EPS : s;
+#endif
+}
+// canonical x for any u64 x (3 VALU)
+__device__ __forceinline__ u64 gl_canon(u64 x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    u64 out, c;
+    u32 sel;
+    asm("v_cmp_lt_u64_e64 %[c], %[pm1], %[x]\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[sel], 0, 1, %[c]\n\t"
+        "v_mad_u64_u32 %[out], %[c], %[sel], -1, %[x]"
+        : [out] "=&v"(out), [sel] "=&v"(sel), [c] "=&s"(c)
+        : [x] "v"(x), [pm1] "s"(P - 1));
+    return out;
+#else
+    return x >= P ? x - P : x;
+#endif
+}
+// a - b as a 64-bit value with the borrow folded once: a - b + p when a < b; for b <= a + p
+// (b < p or b <= a) the result is the exact representative in [0, 2^64)
+__device__ __forceinline__ u64 gl_sub_weak(u64 a, u64 b) {
+    u32 b0, b1, b2, b3;
+    const u32 dl = __builtin_subc((u32)a, (u32)b, 0u, &b0);
+    const u32 dh = __builtin_subc((u32)(a >> 32), (u32)(b >> 32), b0, &b1);
+    const u32 el = __builtin_subc(dl, b1 ? 0xFFFFFFFFu : 0u, 0u, &b2);
+    const u32 eh = __builtin_subc(dh, 0u, b2, &b3);
+    return ((u64)eh << 32) | el;
+}
+// 64x64 -> 128 product as lo + (hi + cv 2^32) 2^64 from four v_mad_u64_u32 (8 VALU):
+// t1 = a0 b1 + (a0 b0 >> 32), t2 = a1 b0 + t1 (carry cv), lo = {lo(a0 b0), lo(t2)}, hi = a1 b1 + hi(t2)
+__device__ __forceinline__ void gl_prod(u64 a, u64 b, u64& lo, u64& hi, u32& cv) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    u64 p, x, t1, t2, s, c;
+    asm("v_mad_u64_u32 %[p], %[s], %[a0], %[b0], 0\n\t"
+        "v_lshrrev_b64 %[x], 32, %[p]\n\t"
+        "v_mad_u64_u32 %[t1], %[s], %[a0], %[b1], %[x]\n\t"
+        "v_mad_u64_u32 %[t2], %[c], %[a1], %[b0], %[t1]\n\t"
+        "v_pk_mov_b32 %[lo], %[p], %[t2] op_sel:[0,0]\n\t"
+        "v_lshrrev_b64 %[x], 32, %[t2]\n\t"
+        "v_mad_u64_u32 %[hi], %[s], %[a1], %[b1], %[x]\n\t"
+        "v_cndmask_b32_e64 %[cv], 0, 1, %[c]"
+        : [p] "=&v"(p), [x] "=&v"(x), [t1] "=&v"(t1), [t2] "=&v"(t2), [lo] "=&v"(lo), [hi] "=&v"(hi),
+          [cv] "=&v"(cv), [s] "=&s"(s), [c] "=&s"(c)
+        : [a0] "v"((u32)a), [a1] "v"((u32)(a >> 32)), [b0] "v"((u32)b), [b1] "v"((u32)(b >> 32)));
+#else
+    const unsigned __int128 m = (unsigned __int128)a * b;
+    lo = (u64)m;
+    hi = (u64)(m >> 64);
+    cv = 0;
+#endif
+}
+
 __host__ __device__ __forceinline__ u64 gl_mul(u64 a, u64 b) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    // 64x64 -> 128 product from four 32x32+64 mads (v_mad_u64_u32), carries folded into the
-    // addends; 22% faster on gfx950 than the compiler's lowering of a * b / __umul64hi
-    const u32 a0 = (u32)a, a1 = (u32)(a >> 32), b0 = (u32)b, b1 = (u32)(b >> 32);
-    const u64 p00 = (u64)a0 * b0;
-    const u64 t1 = (u64)a0 * b1 + (p00 >> 32);
-    const u64 t2 = (u64)a1 * b0 + (u32)t1;
-    const u64 lo = (u64)(u32)p00 | ((u64)(u32)t2 << 32);
-    const u64 hi = (u64)a1 * b1 + ((t1 >> 32) + (t2 >> 32));
-    return gl_reduce(hi, lo);
+    // a b = lo + hl 2^64 + hh 2^96 == lo + hl EPS - hh; (hh + cv) <= 2^32 - 1 for any a, b < 2^64
+    // (18 VALU; the compiler's own lowering of the same math was 24)
+    u64 lo, hi;
+    u32 cv;
+    gl_prod(a, b, lo, hi, cv);
+    const u32 hh = (u32)(hi >> 32) + cv;
+    return gl_fold(gl_sub_weak(lo, hh), (u32)hi);
 #else
     return gl_reduce(mulhi64(a, b), a * b);
 #endif

@@ -28,13 +28,17 @@ namespace xfg {
 // constant after unrolling. Canonical result for canonical x.
 __device__ __forceinline__ u64 mul_pow2(u64 x, int s) {
     if (s == 0) return x;
-    if (s <= 32) return gl_add_small(x << s, ((x >> (64 - s)) << 32) - (x >> (64 - s)));  // hi < 2^32: lo + hi * EPS
-    if (s < 64) return gl_reduce(x >> (64 - s), x << s);
-    // x * 2^(s-64) = v + y * 2^32 with v < 2^32, y = x >> (96 - s) < 2^63; times 2^64 == v * EPS - y
-    const u64 v = (u64)(uint32_t)(x << (s - 64)), y = x >> (96 - s);
-    u64 d;
-    const bool b = __builtin_sub_overflow((v << 32) - v, y, &d);
-    return b ? d - EPS : d;
+    // s <= 32: x 2^s = lo + h 2^64 with h = x >> (64 - s) < 2^32 -> lo + h EPS (6 VALU)
+    if (s <= 32) return gl_fold(x << s, (u32)(x >> 32) >> (32 - s));
+    // 32 < s < 64: h = x >> (64 - s) = hh 2^32 + hl -> lo + hl EPS - hh (11 VALU)
+    if (s < 64) {
+        const u64 h = x >> (64 - s);
+        return gl_fold(gl_sub_weak(x << s, h >> 32), (u32)h);
+    }
+    // x * 2^(s-64) = v + y * 2^32 with v < 2^32, y = x >> (96 - s) < 2^63; times 2^64 == v * EPS - y,
+    // and v EPS < p, y < 2^63 keep the single borrow fold canonical (8 VALU)
+    const u32 v = (u32)x << (s - 64);
+    return gl_sub_weak((u64)v * EPS, x >> (96 - s));
 }
 // exponent of two of w_{2^k} (Winterfell's roots: get_root_of_unity(k))
 __host__ __device__ constexpr int root_exp2(int k) {
@@ -54,8 +58,8 @@ __device__ __forceinline__ u64 add_w(u64 a, u64 b) {  // b < p
     const bool c = __builtin_add_overflow(a, b, &s);
     return s + (c ? EPS : 0);
 }
-__device__ __forceinline__ u64 sub_w(u64 a, u64 b) { return add_w(a, P - b); }  // b < p
-__device__ __forceinline__ u64 canon(u64 x) { return x >= P ? x - P : x; }
+__device__ __forceinline__ u64 sub_w(u64 a, u64 b) { return gl_sub_weak(a, b); }  // b < p
+__device__ __forceinline__ u64 canon(u64 x) { return gl_canon(x); }
 
 // in-register DFT of size 2^LOGR (<= 16): v[q] <- sum_r v[r] w_R^(+-rq), natural order in/out.
 // In: v[r] < p for every r whose bit-reversed position is odd (the level-0 subtrahends: every
@@ -453,6 +457,27 @@ void launch_interpolate(const u64* evals, u64 in_stride, u64* out, u64 out_strid
     a.scale = gl_inv(1ULL << logn);
     a.t4 = (T.fs && logn <= FOURSTEP_MAX_LOG) ? T.fs->inv[logn] : nullptr;
     ntt_run(a, npoly, true, s);
+}
+
+__global__ void field_op_kernel(int op, const u64* a, const u64* b, u64* out, u64 count) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const u64 x = a[i], y = b[i];
+    u64 r = 0;
+    switch (op) {
+        case 0: r = gl_mul(x, y); break;
+        case 1: r = gl_add(x, y); break;
+        case 2: r = gl_sub(x, y); break;
+        case 3: r = gl_canon(x); break;
+        case 4: r = mul_pow2(x, (int)(y % 96)); break;
+        case 5: r = gl_fold(x, (u32)y); break;
+        case 6: r = gl_sub_weak(x, y); break;
+        default: break;
+    }
+    out[i] = r;
+}
+void launch_field_op(int op, const u64* a, const u64* b, u64* out, u64 count, hipStream_t s) {
+    hipLaunchKernelGGL(field_op_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s, op, a, b, out, count);
 }
 
 }  // namespace xfg

@@ -1579,6 +1579,28 @@ int xfg_debug_interpolate(xfg_ctx* c, const uint64_t* evals, uint32_t npoly, uin
     });
 }
 
+int xfg_debug_field(xfg_ctx* c, uint32_t op, uint64_t count, const uint64_t* a, const uint64_t* b, uint64_t* out) {
+    if (!c || !a || !b || !out || op > 6 || count == 0) return XFG_INVALID_ARGUMENT;
+    if (busy(c)) {
+        c->err = "batches pending: call xfg_batch_wait first";
+        return XFG_INVALID_ARGUMENT;
+    }
+    return guarded(c, [&]() -> int {
+        Lane* L = lane0(c);
+        HIPCHK(hipSetDevice(c->device));
+        L->trace.ensure((size_t)count * 3);
+        u64* da = L->trace.p;
+        u64* db = da + count;
+        u64* dout = db + count;
+        HIPCHK(hipMemcpy(da, a, count * 8, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(db, b, count * 8, hipMemcpyHostToDevice));
+        launch_field_op((int)op, da, db, dout, count, L->stream);
+        HIPCHK(hipMemcpyAsync(out, dout, count * 8, hipMemcpyDeviceToHost, L->stream));
+        HIPCHK(hipStreamSynchronize(L->stream));
+        return XFG_OK;
+    });
+}
+
 int xfg_debug_ood_deep(xfg_ctx* c, uint32_t count, uint64_t n, const uint64_t* coef, const uint64_t* hcoef,
                        const uint64_t* zpts, const uint64_t* coeffs, uint64_t* ood_out, uint64_t* deep_out) {
     if (!c || !coef || !hcoef || !zpts || !coeffs || !ood_out || !deep_out || !is_pow2(n) || n < 8 || count == 0)

@@ -85,6 +85,7 @@ _lib.xfg_lde_probe.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double), C.POI
 _lib.xfg_debug_lde.argtypes = [C.c_void_p, _u64p, C.c_uint32, C.c_uint64, C.c_uint32, _u64p]
 _lib.xfg_debug_ood_deep.argtypes = [C.c_void_p, C.c_uint32, C.c_uint64, _u64p, _u64p, _u64p, _u64p, _u64p, _u64p]
 _lib.xfg_debug_interpolate.argtypes = [C.c_void_p, _u64p, C.c_uint32, C.c_uint64, C.c_int, _u64p]
+_lib.xfg_debug_field.argtypes = [C.c_void_p, C.c_uint32, C.c_uint64, _u64p, _u64p, _u64p]
 
 
 class XfgStarkError(Exception):
@@ -521,6 +522,20 @@ class XfgBurnMintProver:
         if st:
             raise self._err(st)
         return ood, deep
+
+    FIELD_OPS = {"mul": 0, "add": 1, "sub": 2, "canon": 3, "pow2": 4, "fold": 5, "sub_weak": 6}
+
+    def debug_field(self, op, a, b):
+        """device Goldilocks primitive `op` (FIELD_OPS) applied elementwise to u64 arrays a, b"""
+        import numpy as np
+        x = np.ascontiguousarray(a, dtype=np.uint64)
+        y = np.ascontiguousarray(b, dtype=np.uint64)
+        out = np.zeros_like(x)
+        st = _lib.xfg_debug_field(self._ctx, self.FIELD_OPS[op], x.size, x.ctypes.data_as(_u64p),
+                                  y.ctypes.data_as(_u64p), out.ctypes.data_as(_u64p))
+        if st:
+            raise self._err(st)
+        return out
 
     def debug_interpolate(self, evals, n, offset7=False):
         import numpy as np
