@@ -107,18 +107,20 @@ def sharded_step(prove_fn, all_inputs, rank, world, per_rank, device, dist):
     return gather_proofs(prove_fn(local), rank, world, per_rank, device, dist)
 
 
-def pipelined_steps(submit_fn, collect_fn, batches, rank, world, per_rank, device, dist, packed=None):
-    """run len(batches) steps with submission depth 2: step i+1's shard is scattered and submitted
-    before step i's proofs are collected and gathered, so one batch's host tail overlaps the next
-    batch's kernels. Every step is proven in full; returns the last step's proofs on rank 0."""
-    pending, out = None, None
+def pipelined_steps(submit_fn, collect_fn, batches, rank, world, per_rank, device, dist, packed=None, depth=2):
+    """run len(batches) steps with `depth` batches in flight: step i+depth-1's shard is scattered
+    and submitted before step i's proofs are collected and gathered, so the host tail of one batch
+    (and the Python collection) overlaps the kernels of the next ones. Every step is proven in
+    full; returns the last step's proofs on rank 0."""
+    pending, out = [], None
     for i, b in enumerate(batches):
         local = scatter_inputs(b, rank, world, per_rank, device, dist, packed[i] if packed else None)
-        nxt = submit_fn(local)
-        if pending is not None:
-            out = gather_proofs(collect_fn(pending), rank, world, per_rank, device, dist)
-        pending = nxt
-    return gather_proofs(collect_fn(pending), rank, world, per_rank, device, dist)
+        pending.append(submit_fn(local))
+        if len(pending) >= depth:
+            out = gather_proofs(collect_fn(pending.pop(0)), rank, world, per_rank, device, dist)
+    while pending:
+        out = gather_proofs(collect_fn(pending.pop(0)), rank, world, per_rank, device, dist)
+    return out
 
 
 def config5(prover, batch=4, calls=5):
@@ -203,6 +205,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-config5", action="store_true", help="skip the configs[4] side measurement")
+    ap.add_argument("--depth", type=int, default=3, help="batches in flight (pipelined submission)")
     args = ap.parse_args()
 
     import torch
@@ -249,12 +252,12 @@ def main():
 
     if args.warmup:
         pipelined_steps(submit_fn, collect_fn, batches[:args.warmup], rank, world, per, device, dist,
-                        packed[:args.warmup] if packed else None)
+                        packed[:args.warmup] if packed else None, args.depth)
     barrier()
     prover.lde_probe(True)  # HIP events around every trace-LDE launch set inside the timed steps
     t0 = time.perf_counter()
     out = pipelined_steps(submit_fn, collect_fn, batches[args.warmup:], rank, world, per, device, dist,
-                          packed[args.warmup:] if packed else None)
+                          packed[args.warmup:] if packed else None, args.depth)
     barrier()
     el = time.perf_counter() - t0
     el_t = torch.tensor([el], dtype=torch.float64, device=device)
@@ -304,7 +307,7 @@ def main():
                 "trace_length": n, "blowup": BLOWUP, "proof_options": "42/8/4/None/8/31",
                 "proofs_per_step": per * world,
                 "parallelism": f"dp{world} (independent proofs; RCCL scatter of inputs, gather of proof bytes)",
-                "submission": "pipelined, depth 2 (xfg_prove_batch_submit / xfg_batch_wait)",
+                "submission": f"pipelined, depth {args.depth} (xfg_prove_batch_submit / xfg_batch_wait)",
             },
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,

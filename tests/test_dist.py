@@ -49,8 +49,9 @@ def _worker(rank, world, port, per, ret, mode="sync"):
             seen.append(len(kws))
             return _fake_prove(kws)
 
+        depth = 3 if mode == "pipelined3" else 2
         out = bench.pipelined_steps(submit, lambda p: p, batches, rank, world, per, torch.device("cpu"), dist,
-                                    packed)
+                                    packed, depth)
         assert seen == [per] * 3
     if rank == 0:
         ret.put(out)
@@ -68,7 +69,7 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("world,per,mode", [(2, 3, "sync"), (2, 1, "sync"), (2, 2, "pipelined")])
+@pytest.mark.parametrize("world,per,mode", [(2, 3, "sync"), (2, 1, "sync"), (2, 2, "pipelined"), (2, 2, "pipelined3")])
 def test_sharded_step_gloo(world, per, mode):
     import synthetic
     ctx = mp.get_context("spawn")
@@ -81,7 +82,7 @@ def test_sharded_step_gloo(world, per, mode):
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    base = 200 if mode == "pipelined" else 0  # pipelined: the last of 3 steps
+    base = 200 if mode.startswith("pipelined") else 0  # pipelined: the last of 3 steps
     want = _fake_prove([synthetic.burn_inputs(base + i) for i in range(per * world)])
     assert out == want
 
