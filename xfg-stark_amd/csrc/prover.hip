@@ -130,8 +130,12 @@ static int marshal(const xfg_burn_inputs* in, AirConst& a, std::string& err) {
 
 // ------------------------------------------------------------------ byte writer
 struct BW {
-    std::vector<uint8_t> b;
+    std::vector<uint8_t>& b;  // caller-owned scratch, reused across proofs (never shrunk)
     size_t o = 0;
+    explicit BW(std::vector<uint8_t>& buf) : b(buf) {}
+    void reserve(size_t k) {
+        if (b.size() < k) b.resize(k);
+    }
     uint8_t* at(size_t k) {  // k bytes at the cursor (grows geometrically; callers pre-size)
         if (o + k > b.size()) b.resize(std::max(2 * b.size(), o + k));
         uint8_t* q = b.data() + o;
@@ -150,10 +154,7 @@ struct BW {
         uint32_t x = (uint32_t)(o - end_of_slot);
         memcpy(b.data() + end_of_slot - 4, &x, 4);
     }
-    void finish(std::vector<uint8_t>& out) {
-        b.resize(o);
-        out.swap(b);
-    }
+    void finish(std::vector<uint8_t>& out) { out.assign(b.begin(), b.begin() + o); }
 };
 
 // ------------------------------------------------------------------ device buffers
@@ -270,6 +271,13 @@ struct Lane {
     HBuf<u64> h_co, h_zp, h_ood, h_a7, h_rem, h_dn2, h_idx, h_gv;
     HBuf<AirConst> h_air;
     HBuf<DeepParams> h_dp;
+    // host scratch of the opening plans and the serialiser, kept across units so steady-state
+    // units neither allocate nor page-fault (their cost grew with the shared hosts' load)
+    struct {
+        std::vector<u64> vidx_lde, vidx_h, didx_t, didx_h, open_ent, allidx;
+        std::vector<std::vector<u64>> vidx_f, didx_f;
+        std::vector<uint8_t> ser;
+    } hs;
     void release() {
         for (auto* b : {&h_roots, &h_gd}) b->release();
         for (auto* b : {&h_co, &h_zp, &h_ood, &h_a7, &h_rem, &h_dn2, &h_idx, &h_gv}) b->release();
@@ -705,8 +713,22 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     // LDE trees store heap levels >= log2(beta) (indices < 2n); lower nodes of an opened row are
     // recomputed by launch_open_rows (local heap: 2 * beta slots per row)
     const u64 stored_lim = n, LB = beta;  // stored: heap levels >= log2(beta) + 1
-    std::vector<u64> vidx_lde, vidx_h, didx_t, didx_h, open_ent;
-    std::vector<std::vector<u64>> vidx_f(nl + 1), didx_f(nl + 1);
+    auto& vidx_lde = c->hs.vidx_lde;
+    auto& vidx_h = c->hs.vidx_h;
+    auto& didx_t = c->hs.didx_t;
+    auto& didx_h = c->hs.didx_h;
+    auto& open_ent = c->hs.open_ent;
+    auto& vidx_f = c->hs.vidx_f;
+    auto& didx_f = c->hs.didx_f;
+    for (auto* v : {&vidx_lde, &vidx_h, &didx_t, &didx_h, &open_ent}) v->clear();
+    if (vidx_f.size() < nl + 1) {
+        vidx_f.resize(nl + 1);
+        didx_f.resize(nl + 1);
+    }
+    for (unsigned l = 0; l <= nl; l++) {
+        vidx_f[l].clear();
+        didx_f[l].clear();
+    }
     struct Layout {
         BatchOpening op;                     // trace / constraint trees (same positions)
         std::vector<int64_t> ref;            // per node: >= 0 stored ordinal, < 0 -(open slot + 1)
@@ -798,7 +820,8 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     }
     ht.mark("queries_plan");
     // one index buffer, one value buffer, one digest buffer; segment per source
-    std::vector<u64> allidx;
+    auto& allidx = c->hs.allidx;
+    allidx.clear();
     std::vector<std::pair<size_t, size_t>> vseg, dseg;  // (offset, count)
     auto add_seg = [&](const std::vector<u64>& v, std::vector<std::pair<size_t, size_t>>& seg) {
         seg.push_back({allidx.size(), v.size()});
@@ -819,7 +842,9 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     c->gdig.ensure(ndig + 2 * nopen);
     u64* hidx = c->h_idx.ensure(allidx.size());
     memcpy(hidx, allidx.data(), allidx.size() * 8);
+    ht.mark("q_idx_host");
     HIPCHK(hipMemcpyAsync(c->gidx.p, hidx, allidx.size() * 8, hipMemcpyHostToDevice, s));
+    ht.mark("q_h2d");
     {
         size_t vo = 0;
         const u64* vsrc[2] = {c->lde.p, c->hlde.p};
@@ -838,6 +863,7 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         launch_open_rows(c->lde.p, 7, ent, nent, c->gdig.p + ndig, logn, logbeta, s);
         launch_open_rows(c->hlde.p, DE, ent, nent, c->gdig.p + ndig + nopen, logn, logbeta, s);
     }
+    ht.mark("q_launch");
     u64* gv = c->h_gv.ensure(nvals);
     Digest* gd = c->h_gd.ensure(ndig + 2 * nopen);
     if (nvals) HIPCHK(hipMemcpyAsync(gv, c->gval.p, nvals * 8, hipMemcpyDeviceToHost, s));
@@ -888,8 +914,8 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     for (int b = 0; b < B; b++) {
         auto& j = jobs[b];
         const u64 nu = j.pos.size();
-        BW w;
-        w.b.resize(j.commitments.size() + nu * 8 * (7 + DE + 8 * DE * nl) + (2 + nl) * nu * 32 * ilog2(N) +
+        BW w(c->hs.ser);
+        w.reserve(j.commitments.size() + nu * 8 * (7 + DE + 8 * DE * nl) + (2 + nl) * nu * 32 * ilog2(N) +
                    rem_len * 8 * DE + 1024);
         // Context
         w.u8(7); w.u8(0); w.u8(logn); w.u16(0);
