@@ -213,14 +213,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # XFG_DIST_BACKEND=gloo rehearses the N > 1 path on a box with fewer GPUs than ranks: the ranks
+    # share the visible GPUs round-robin and the scatter / gather tensors stay on the host
+    backend = os.environ.get("XFG_DIST_BACKEND", "nccl")
+    gpu = local_rank % max(1, torch.cuda.device_count()) if backend != "nccl" else local_rank
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
-    device = torch.device("cuda", local_rank)
+        torch.cuda.set_device(gpu)
+        dist.init_process_group(backend)
+    device = torch.device("cuda", gpu) if backend == "nccl" else torch.device("cpu")
 
     import xfgstark
-    prover = xfgstark.XfgBurnMintProver(device=local_rank)
+    prover = xfgstark.XfgBurnMintProver(device=gpu)
     n = 1 << args.log_n
     per = args.per_gpu
     prover.prepare(per, n)  # workspace allocation + code-object load (setup, not a proving step)
@@ -248,7 +252,7 @@ def main():
     def barrier():
         if dist is not None:
             dist.barrier()
-        torch.cuda.synchronize()
+        torch.cuda.synchronize(gpu)
 
     if args.warmup:
         pipelined_steps(submit_fn, collect_fn, batches[:args.warmup], rank, world, per, device, dist,
