@@ -157,6 +157,16 @@ struct BW {
     void finish(std::vector<uint8_t>& out) { out.assign(b.begin(), b.begin() + o); }
 };
 
+// XFG_TRACE=1: host-side phase timestamps of every prove call (and any workspace reallocation,
+// which synchronises the device), printed to stderr
+static bool trace_on() {
+    static const bool on = getenv("XFG_TRACE") && *getenv("XFG_TRACE") == '1';
+    return on;
+}
+static void trace_realloc(const char* kind, size_t old_n, size_t new_n, size_t elem) {
+    if (trace_on()) fprintf(stderr, "[xfg] realloc %s %zu -> %zu bytes\n", kind, old_n * elem, new_n * elem);
+}
+
 // ------------------------------------------------------------------ device buffers
 template <class T>
 struct DBuf {
@@ -164,6 +174,7 @@ struct DBuf {
     size_t n = 0;
     void ensure(size_t cnt) {
         if (cnt <= n) return;
+        trace_realloc("device", n, std::max<size_t>(cnt + cnt / 8, 1), sizeof(T));
         if (p) (void)hipFree(p);
         p = nullptr;
         n = 0;
@@ -185,6 +196,7 @@ struct HBuf {
     size_t n = 0;
     T* ensure(size_t cnt) {
         if (cnt <= n) return p;
+        trace_realloc("pinned", n, cnt + cnt / 4 + 16, sizeof(T));
         if (p) (void)hipHostFree(p);
         p = nullptr;
         n = 0;
@@ -426,11 +438,6 @@ struct ProofJob {
 
 static void stage_mark(Lane* c, int k) {
     if (c->timing) HIPCHK(hipEventRecord(c->ev[k], c->stream));
-}
-// XFG_TRACE=1: host-side phase timestamps of every prove call, printed to stderr
-static bool trace_on() {
-    static const bool on = getenv("XFG_TRACE") && *getenv("XFG_TRACE") == '1';
-    return on;
 }
 struct HostTrace {
     std::vector<std::pair<const char*, std::chrono::steady_clock::time_point>> m;
