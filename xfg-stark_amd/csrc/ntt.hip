@@ -19,26 +19,56 @@
 // (LDS table per coset) and a post-factor 7^j2 w_N^(j2 t) folded into the four-step twiddle.
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
+#include <utility>
 #include "kernels.hpp"
 
 namespace xfg {
 
 // ---------------------------------------------------------------- shift-based multiplies
-// x * 2^s mod p for 0 <= s < 96 (2^96 == -1 is handled by the caller); s is a compile-time
-// constant after unrolling. Canonical result for canonical x.
-__device__ __forceinline__ u64 mul_pow2(u64 x, int s) {
-    if (s == 0) return x;
-    // s <= 32: x 2^s = lo + h 2^64 with h = x >> (64 - s) < 2^32 -> lo + h EPS (6 VALU)
-    if (s <= 32) return gl_fold(x << s, (u32)(x >> 32) >> (32 - s));
-    // 32 < s < 64: h = x >> (64 - s) = hh 2^32 + hl -> lo + hl EPS - hh (11 VALU)
-    if (s < 64) {
-        const u64 h = x >> (64 - s);
-        return gl_fold(gl_sub_weak(x << s, h >> 32), (u32)h);
+// compile-time loops (C++17): f(std::integral_constant<int, I>) for I = 0 .. N-1, so shift amounts
+// and twiddle exponents are constants at the AST level (the asm "i" operands below need that)
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+// 64-bit shifts as one v_lshlrev_b64 / v_lshrrev_b64 (the compiler splits a 64-bit shift into
+// v_alignbit_b32 + a 32-bit shift: two issue slots at the same rate as the one 64-bit op)
+template <int S>
+__device__ __forceinline__ u64 shl64(u64 x) {
+    u64 r;
+    asm("v_lshlrev_b64 %0, %1, %2" : "=v"(r) : "i"(S), "v"(x));
+    return r;
+}
+template <int S>
+__device__ __forceinline__ u64 shr64(u64 x) {
+    u64 r;
+    asm("v_lshrrev_b64 %0, %1, %2" : "=v"(r) : "i"(S), "v"(x));
+    return r;
+}
+// x * 2^S mod p for 0 <= S < 96 (2^96 == -1 is handled by the caller). Canonical result for any
+// u64 x when S > 0; S == 0 returns x as is.
+template <int S>
+__device__ __forceinline__ u64 mul_pow2(u64 x) {
+    if constexpr (S == 0) {
+        return x;
+    } else if constexpr (S <= 32) {
+        // x 2^S = lo + h 2^64 with h = x >> (64 - S) < 2^32 -> lo + h EPS
+        return gl_fold(shl64<S>(x), (u32)(x >> 32) >> (32 - S));
+    } else if constexpr (S < 64) {
+        // h = x >> (64 - S) = hh 2^32 + hl -> lo + hl EPS - hh
+        const u64 h = shr64<64 - S>(x);
+        return gl_fold(gl_sub_weak(shl64<S>(x), h >> 32), (u32)h);
+    } else {
+        // x * 2^(S-64) = v + y * 2^32 with v < 2^32, y = x >> (96 - S) < 2^63; times 2^64 == v * EPS - y,
+        // and v EPS < p, y < 2^63 keep the single borrow fold canonical
+        const u32 v = (u32)x << (S - 64);
+        return gl_sub_weak((u64)v * EPS, shr64<96 - S>(x));
     }
-    // x * 2^(s-64) = v + y * 2^32 with v < 2^32, y = x >> (96 - s) < 2^63; times 2^64 == v * EPS - y,
-    // and v EPS < p, y < 2^63 keep the single borrow fold canonical (8 VALU)
-    const u32 v = (u32)x << (s - 64);
-    return gl_sub_weak((u64)v * EPS, x >> (96 - s));
 }
 // exponent of two of w_{2^k} (Winterfell's roots: get_root_of_unity(k))
 __host__ __device__ constexpr int root_exp2(int k) {
@@ -53,10 +83,19 @@ __host__ __device__ constexpr int brev_c(int x, int bits) {
 // Weakly reduced values: any u64 congruent mod p. The butterflies keep their outputs weak and
 // reduce only the subtrahend / addend t (which must be < p for these forms): u + t carries at most
 // once past 2^64 when t < p, and u - t borrows into a value >= EPS when t < p.
+// u + t as s = u + t plus (carry) EPS via one v_mad_u64_u32 (4 VALU; the compiler's form built a
+// {mask, 0} register pair with a v_mov for every add)
 __device__ __forceinline__ u64 add_w(u64 a, u64 b) {  // b < p
-    u64 s;
-    const bool c = __builtin_add_overflow(a, b, &s);
-    return s + (c ? EPS : 0);
+    u64 s, out, c;
+    u32 sel;
+    asm("v_lshl_add_u64 %[s], %[a], 0, %[b]\n\t"
+        "v_cmp_lt_u64_e64 %[c], %[s], %[b]\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[sel], 0, 1, %[c]\n\t"
+        "v_mad_u64_u32 %[out], %[c], %[sel], -1, %[s]"
+        : [s] "=&v"(s), [out] "=&v"(out), [sel] "=&v"(sel), [c] "=&s"(c)
+        : [a] "v"(a), [b] "v"(b));
+    return out;
 }
 __device__ __forceinline__ u64 sub_w(u64 a, u64 b) { return gl_sub_weak(a, b); }  // b < p
 __device__ __forceinline__ u64 canon(u64 x) { return gl_canon(x); }
@@ -71,26 +110,29 @@ __device__ __forceinline__ void dft_reg(u64* v) {
     u64 a[R];
 #pragma unroll
     for (int i = 0; i < R; i++) a[i] = v[brev_c(i, LOGR)];
-#pragma unroll
-    for (int s = 0; s < LOGR; s++) {
-        const int h = 1 << s;
-#pragma unroll
-        for (int b = 0; b < R / 2; b++) {
-            const int pos = b & (h - 1), i0 = ((b >> s) << (s + 1)) + pos;
-            int e = (root_exp2(s + 1) * pos) % 192;
-            if (INV && e) e = 192 - e;
+    static_for<LOGR>([&](auto sc) {
+        constexpr int s = decltype(sc)::value, h = 1 << s;
+        static_for<R / 2>([&](auto bc) {
+            constexpr int b = decltype(bc)::value;
+            constexpr int pos = b & (h - 1), i0 = ((b >> s) << (s + 1)) + pos;
+            constexpr int e0 = (root_exp2(s + 1) * pos) % 192;
+            constexpr int e = (INV && e0) ? 192 - e0 : e0;
             // w = 2^e = -2^(e - 96) for e >= 96: the sign swaps the butterfly's add and sub
             const u64 x = a[i0 + h];
-            const u64 t = (e % 96) ? mul_pow2(x, e % 96) : (s == 0 ? x : canon(x)), u = a[i0];
-            if (e >= 96) {
+            u64 t;
+            if constexpr (e % 96 != 0) t = mul_pow2<e % 96>(x);
+            else if constexpr (s == 0) t = x;
+            else t = canon(x);
+            const u64 u = a[i0];
+            if constexpr (e >= 96) {
                 a[i0] = sub_w(u, t);
                 a[i0 + h] = add_w(u, t);
             } else {
                 a[i0] = add_w(u, t);
                 a[i0 + h] = sub_w(u, t);
             }
-        }
-    }
+        });
+    });
 #pragma unroll
     for (int i = 0; i < R; i++) v[i] = a[i];
 }
@@ -469,7 +511,13 @@ __global__ void field_op_kernel(int op, const u64* a, const u64* b, u64* out, u6
         case 1: r = gl_add(x, y); break;
         case 2: r = gl_sub(x, y); break;
         case 3: r = gl_canon(x); break;
-        case 4: r = mul_pow2(x, (int)(y % 96)); break;
+        case 4: {
+            const int sh = (int)(y % 96);
+            static_for<96>([&](auto sc) {
+                if (sh == decltype(sc)::value) r = mul_pow2<decltype(sc)::value>(x);
+            });
+            break;
+        }
         case 5: r = gl_fold(x, (u32)y); break;
         case 6: r = gl_sub_weak(x, y); break;
         default: break;
