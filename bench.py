@@ -163,15 +163,32 @@ def in_pipeline(ms, sets, polys, n):
             "achieved_GBps": round(b / (ms * 1e-3) / 1e9, 1)}
 
 
-def pmc_traffic(per, n, blowup):
-    """HBM bytes per trace-LDE launch set from the committed PMC pass (profiles/rNN/lde_pmc.json,
-    made by scripts/profile_round.sh: FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 --pmc runs)"""
+def pmc_record(per, n, blowup):
+    """the committed PMC record of the trace-LDE launch set (profiles/rNN/lde_pmc.json, made by
+    scripts/profile_round.sh: FETCH_SIZE x2 + WRITE_SIZE and SQ_INSTS_VALU, separate rocprofv3 --pmc
+    runs) and its path, or (None, None)"""
     import glob
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "lde_pmc.json")), reverse=True):
         d = json.load(open(f))
         if (d.get("count"), d.get("n"), d.get("blowup")) == (per, n, blowup):
-            return d["traffic_bytes"], os.path.relpath(f, ROOT)
+            return d, os.path.relpath(f, ROOT)
     return None, None
+
+
+VALU_HALF_RATE_T = 36.0  # measured issue ceiling of the 64-bit / carry VALU forms (scripts/ubench/valu_ubench.hip)
+
+
+def valu_roofline(rec, lde_ms, outputs):
+    """the bound that actually holds for the NTT: VALU issue. Lane-instructions per output from the
+    PMC wave-instruction counts (x64 lanes), and the achieved issue rate at the measured launch-set
+    time against the half-rate ceiling the Goldilocks carry / 64-bit forms run at"""
+    if not rec or not rec.get("valu_insts_pass_a"):
+        return None
+    lane_instr = 64.0 * (rec["valu_insts_pass_a"] + rec["valu_insts_pass_b"])
+    rate = lane_instr / (lde_ms * 1e-3) / 1e12
+    return {"lane_instr_per_output": round(lane_instr / outputs, 1), "achieved_T_lane_instr_s": round(rate, 2),
+            "ceiling_T_lane_instr_s": VALU_HALF_RATE_T, "frac": round(rate / VALU_HALF_RATE_T, 3),
+            "valu_busy_pct": [rec.get("valu_busy_pct_pass_a"), rec.get("valu_busy_pct_pass_b")]}
 
 
 def cpu_baseline(seconds=10.0):
@@ -282,7 +299,8 @@ def main():
     lde_ms = prover.bench_lde(per, n, BLOWUP, 10)
     lde_bytes = 8 * WIDTH * (n + n * BLOWUP) * per
     achieved = lde_bytes / (lde_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(per, n, BLOWUP)
+    pmc, traffic_src = pmc_record(per, n, BLOWUP)
+    traffic = pmc["traffic_bytes"] if pmc else None
     prover.set_timing(True)
     prover_stage = {}
     if rank == 0:
@@ -316,6 +334,9 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
                          "traffic_source": traffic_src,
+                         # the kernel is VALU-issue-bound: the same launch set
+                         # against the VALU ceiling, instruction counts from the same PMC record
+                         "valu": valu_roofline(pmc, lde_ms, WIDTH * per * n * BLOWUP),
                          "kernel": "trace LDE (ntt_pass_a<8,false> + ntt_pass_b<8,false>), 7 columns x "
                                    f"{per} proofs, {lde_ms:.3f} ms/launch-set, {lde_bytes} algorithmic B",
                          # the same launch sets inside the timed pipelined steps (per 16-proof unit,

@@ -11,7 +11,8 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _PKG = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(_PKG, "libxfgstark.so")
+# XFG_LIB: an alternative build of the same library (same-box A/B of kernel variants)
+LIB_PATH = os.environ.get("XFG_LIB") or os.path.join(_PKG, "libxfgstark.so")
 HEADER_PATH = os.path.join(os.path.dirname(_PKG), "include", "xfg_stark.h")
 
 if not os.path.exists(LIB_PATH):
@@ -85,7 +86,8 @@ _lib.xfg_lde_probe.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double), C.POI
 _lib.xfg_debug_lde.argtypes = [C.c_void_p, _u64p, C.c_uint32, C.c_uint64, C.c_uint32, _u64p]
 _lib.xfg_debug_ood_deep.argtypes = [C.c_void_p, C.c_uint32, C.c_uint64, _u64p, _u64p, _u64p, _u64p, _u64p, _u64p]
 _lib.xfg_debug_interpolate.argtypes = [C.c_void_p, _u64p, C.c_uint32, C.c_uint64, C.c_int, _u64p]
-_lib.xfg_debug_field.argtypes = [C.c_void_p, C.c_uint32, C.c_uint64, _u64p, _u64p, _u64p]
+if hasattr(_lib, "xfg_debug_field"):  # absent from builds older than the primitive self test (XFG_LIB A/B)
+    _lib.xfg_debug_field.argtypes = [C.c_void_p, C.c_uint32, C.c_uint64, _u64p, _u64p, _u64p]
 
 
 class XfgStarkError(Exception):
