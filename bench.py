@@ -73,30 +73,47 @@ def scatter_inputs(all_inputs, rank, world, per_rank, device, dist, packed=None)
 
 
 def gather_proofs(proofs, rank, world, per_rank, device, dist):
-    """this rank's proof bytes -> all proofs on rank 0 (None elsewhere): lengths, then padded
-    buffers, over the process group"""
+    """this rank's proof bytes -> all proofs on rank 0 (None elsewhere) over the process group: one
+    gather of [per_rank int64 lengths | concatenated proofs], padded to the longest rank payload;
+    rank 0 gets zero-copy memoryviews into the gathered buffer (one D2H for all ranks into a reused
+    pinned buffer: the views stay valid until the next call)"""
     import numpy as np
     import torch
     if world == 1:
         return proofs
-    lens = torch.tensor([len(p) for p in proofs], dtype=torch.int64, device=device)
-    maxlen = torch.tensor([max(len(p) for p in proofs)], dtype=torch.int64, device=device)
-    dist.all_reduce(maxlen, op=dist.ReduceOp.MAX)
-    L = int(maxlen.item())
-    buf = np.zeros((per_rank, L), dtype=np.uint8)
-    for i, p in enumerate(proofs):
-        buf[i, :len(p)] = np.frombuffer(p, dtype=np.uint8)
-    tbuf = torch.from_numpy(buf).to(device)
-    glens = [torch.empty_like(lens) for _ in range(world)] if rank == 0 else None
-    gbufs = [torch.empty_like(tbuf) for _ in range(world)] if rank == 0 else None
-    dist.gather(lens, glens, dst=0)
-    dist.gather(tbuf, gbufs, dst=0)
+    lens = np.array([len(p) for p in proofs], dtype=np.int64)
+    hdr = 8 * per_rank
+    size = torch.tensor([hdr + int(lens.sum())], dtype=torch.int64, device=device)
+    dist.all_reduce(size, op=dist.ReduceOp.MAX)
+    payload = np.zeros(int(size.item()), dtype=np.uint8)
+    payload[:hdr] = lens.view(np.uint8)
+    off = hdr
+    for p in proofs:  # one copy of each proof, straight into the payload
+        payload[off:off + len(p)] = np.frombuffer(p, dtype=np.uint8)
+        off += len(p)
+    t = torch.from_numpy(payload).to(device)
+    got = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
+    dist.gather(t, got, dst=0)
     if rank != 0:
         return None
+    stacked = torch.stack(got)
+    if stacked.is_cuda:  # one D2H into a reused pinned buffer
+        pin = getattr(gather_proofs, "_pin", None)
+        if pin is None or pin.numel() < stacked.numel():
+            pin = torch.empty(stacked.numel() + (1 << 20), dtype=torch.uint8, pin_memory=True)
+            gather_proofs._pin = pin
+        host = pin[:stacked.numel()].view(stacked.shape)
+        host.copy_(stacked)
+        allb = host.numpy()
+    else:
+        allb = stacked.numpy()
     out = []
     for r in range(world):
-        lr, br = glens[r].cpu().numpy(), gbufs[r].cpu().numpy()
-        out += [bytes(br[i, :lr[i]]) for i in range(per_rank)]
+        row = allb[r]
+        mv, off = memoryview(row), hdr
+        for ln in row[:hdr].view(np.int64):
+            out.append(mv[off:off + int(ln)])
+            off += int(ln)
     return out
 
 

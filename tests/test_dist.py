@@ -54,7 +54,7 @@ def _worker(rank, world, port, per, ret, mode="sync"):
                                     packed, depth)
         assert seen == [per] * 3
     if rank == 0:
-        ret.put(out)
+        ret.put([bytes(x) for x in out])  # rank 0 holds zero-copy views into the gathered buffer
     else:
         assert out is None
     dist.barrier()
@@ -92,3 +92,47 @@ def test_pack_unpack_roundtrip():
     import synthetic
     kws = [synthetic.burn_inputs(i) for i in range(5)] + [synthetic.REFERENCE_PACKAGE]
     assert bench.unpack_inputs(bench.pack_inputs(kws)) == kws
+
+
+class _LoopbackDist:
+    """two "ranks" in one process: rank 1's payload is handed to rank 0's gather (exercises the
+    device-tensor branch of bench.gather_proofs on one GPU)"""
+    class ReduceOp:
+        MAX = "max"
+
+    def __init__(self, other):
+        self.other = other
+
+    def all_reduce(self, t, op=None):
+        t.copy_(torch_max(t, self.other["size"]))
+
+    def gather(self, t, got, dst=0):
+        got[0].copy_(t)
+        got[1].copy_(self.other["payload"].to(t.device))
+
+
+def torch_max(a, b):
+    import torch
+    return torch.maximum(a, b.to(a.device))
+
+
+@pytest.mark.gpu
+def test_gather_proofs_device_branch():
+    import sys
+    import numpy as np
+    import torch
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    per = 3
+    mine = [bytes([i]) * (100 + 37 * i) for i in range(per)]
+    theirs = [bytes([50 + i]) * (300 - 11 * i) for i in range(per)]
+    # rank 1's payload as gather_proofs builds it, padded to the common size
+    hdr = 8 * per
+    size = max(hdr + sum(map(len, mine)), hdr + sum(map(len, theirs)))
+    pay = np.zeros(size, dtype=np.uint8)
+    pay[:hdr] = np.array([len(p) for p in theirs], dtype=np.int64).view(np.uint8)
+    pay[hdr:hdr + sum(map(len, theirs))] = np.frombuffer(b"".join(theirs), dtype=np.uint8)
+    other = {"size": torch.tensor([size], dtype=torch.int64), "payload": torch.from_numpy(pay)}
+    out = bench.gather_proofs(mine, 0, 2, per, torch.device("cuda", 0), _LoopbackDist(other))
+    assert [bytes(x) for x in out] == mine + theirs
