@@ -256,8 +256,26 @@ struct NttArgs {
     u64 scale;    // inverse: n^-1
     u64 keep;     // inverse: coefficients written
     const u64* t4;  // four-step twiddle table (FourStep) or nullptr
+    int xcd;        // 1: XCD-contiguous block order (see xcd_block)
     Tables T;
 };
+
+// Workgroups are dealt round-robin over the 8 XCDs, each with its own L2. When a pass writes less
+// than a 128 B line per tile row, the neighbouring tiles that fill the rest of each line must run
+// on the same XCD at about the same time or every line reaches HBM in pieces: renumber so that
+// XCD x executes the x-th contiguous eighth of the (tile, poly) blocks in order.
+__device__ __forceinline__ void xcd_block(bool on, int& bx, int& by) {
+    if (!on) {
+        bx = blockIdx.x;
+        by = blockIdx.y;
+        return;
+    }
+    const int total = gridDim.x * gridDim.y, L = blockIdx.x + gridDim.x * blockIdx.y;
+    const int per = total >> 3, rem = total & 7, x = L & 7, slot = L >> 3;
+    const int l = (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + slot;
+    bx = l % gridDim.x;
+    by = l / gridDim.x;
+}
 
 // ---------------------------------------------------------------- pass A: column DFTs (size R)
 // forward, coset t: x[j1] = c[C j1 + j2] * 7^(C j1) w_(beta R)^(t j1)
@@ -273,7 +291,9 @@ __global__ __launch_bounds__(THREADS, 4) void ntt_pass_a(NttArgs a) {
     u64* ltw = lds + TC * PITCH;
     u64* pre = ltw + R;  // forward: 7^(C j1) w_(beta R)^(t j1) for this block's coset
     // one block per (column tile, poly, coset); y is [poly][coset][R][C]
-    const int pt = blockIdx.y, col0 = blockIdx.x * TC;
+    int bx, by;
+    xcd_block(a.xcd & 1, bx, by);
+    const int pt = by, col0 = bx * TC;
     const int poly = INV ? pt : (pt >> a.logbeta), t = INV ? 0 : (pt & ((1 << a.logbeta) - 1));
     const u64 n = 1ULL << a.logn;
     const int logN = a.logn + a.logbeta;
@@ -335,7 +355,9 @@ __global__ __launch_bounds__(THREADS) void ntt_pass_b(NttArgs a) {
     const int TR = 1 << logTR;
     u64* tile = lds;
     u64* ltw = lds + TR * row_pitch(C);
-    const int pt = blockIdx.y, k10 = blockIdx.x * TR;
+    int bx, by;
+    xcd_block(a.xcd & 2, bx, by);
+    const int pt = by, k10 = bx * TR;
     const u64 n = 1ULL << a.logn;
     for (int i = threadIdx.x; i < C; i += THREADS) ltw[i] = tw_get(a.T, LOGC, i, INV);
     __syncthreads();
@@ -443,6 +465,13 @@ static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
     size_t lds_a = ((size_t)(1 << logTC) * row_pitch(R) + 2 * R) * sizeof(u64);
     size_t lds_b = ((size_t)(1 << logTR) * row_pitch(C) + C) * sizeof(u64);
     dim3 ga(C >> logTC, npoly * ncos), gb(R >> logTR, npoly * ncos);
+    // tile rows narrower than 16 words (a 128 B line) in the scattered writes: pass A stores TC
+    // consecutive words per row, pass B TR (XFG_NTT_XCD=0 disables, for A/B runs)
+    static const bool xcd_on = [] {
+        const char* v = getenv("XFG_NTT_XCD");
+        return !(v && *v == '0');
+    }();
+    a.xcd = xcd_on ? ((logTC < 4 ? 1 : 0) | (logTR < 4 ? 2 : 0)) : 0;
     if (inv) {
         run_pass_a<true>(a.logR, ga, lds_a, s, a);
         run_pass_b<true>(a.logC, gb, lds_b, s, a);
