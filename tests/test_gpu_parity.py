@@ -45,7 +45,7 @@ def with_blowup(prover, b):
 
 
 @pytest.mark.parametrize("n,blowup", [(8, 2), (64, 8), (256, 16), (1024, 4), (4096, 8), (1 << 15, 8), (1 << 16, 2),
-                                      (1 << 17, 2), (1 << 20, 2)])
+                                      (1 << 17, 2), (1 << 19, 2), (1 << 20, 2), (1 << 21, 2)])
 def test_lde_kernel_matches_oracle(prover, n, blowup):
     rng = np.random.default_rng(n + blowup)
     coef = rng.integers(0, P, size=(3, n), dtype=np.uint64)
@@ -105,7 +105,7 @@ def test_field_primitives_match_bigint(prover, op):
 
 
 @pytest.mark.parametrize("n,off7", [(8, False), (64, True), (2048, False), (2048, True), (1 << 14, True),
-                                    (1 << 17, True), (1 << 20, False)])
+                                    (1 << 17, True), (1 << 19, True), (1 << 20, False), (1 << 21, True)])
 def test_interpolate_kernel_matches_oracle(prover, n, off7):
     rng = np.random.default_rng(n)
     ev = rng.integers(0, P, size=(2, n), dtype=np.uint64)

@@ -137,7 +137,6 @@ __device__ __forceinline__ void dft_reg(u64* v) {
     for (int i = 0; i < R; i++) v[i] = a[i];
 }
 
-constexpr int THREADS = 256;
 // LDS tile: row `seq` of length S at seq * PITCH; element i at i + (i >> 4). The pad word per 16
 // elements makes the stride-16 stores of a first step conflict-free; the odd pitch does the same
 // for lanes walking across rows.
@@ -158,7 +157,7 @@ __device__ __forceinline__ u64 tw_get(const Tables& T, int k, u64 e, bool inv) {
 // outputs of a group, which belong at logical positions base + r * stride.
 // IN_PLACE: every load of the step completes (barrier) before any store.
 // pf(q, seq, base, stride) runs before the group's loads (prefetch of what st will need).
-template <int LOGS, int LOGR, bool INV, bool SEQ_FAST, bool IN_PLACE, class LD, class ST, class PF>
+template <int LOGS, int LOGR, bool INV, bool SEQ_FAST, bool IN_PLACE, int NT, class LD, class ST, class PF>
 __device__ __forceinline__ void stockham(int lognseq, int Ns, const u64* ltw, LD ld, ST st, PF pf) {
     constexpr int S = 1 << LOGS, R = 1 << LOGR, G = S / R, PER = 16 / R;
     const int nseq = 1 << lognseq;
@@ -167,7 +166,7 @@ __device__ __forceinline__ void stockham(int lognseq, int Ns, const u64* ltw, LD
     int gs[PER], gj[PER];
 #pragma unroll
     for (int q = 0; q < PER; q++) {
-        const int g = threadIdx.x + THREADS * q;
+        const int g = threadIdx.x + NT * q;
         gs[q] = -1;
         gj[q] = 0;
         if (g < groups) {
@@ -196,28 +195,32 @@ __device__ __forceinline__ void stockham(int lognseq, int Ns, const u64* ltw, LD
     }
 }
 
-// steps of a size-2^LOGS DFT: the remainder radix first, then radix 16
+// steps of a size-2^LOGS DFT: the remainder radix first, then radix 16. (Remainder last would
+// save general twiddle multiplies -- radix 2 last multiplies 1/2 of the elements where radix 2
+// first makes the next radix-16 step multiply 15/16 -- but its narrow final step stores measured
+// 25 % slower at 2^20: 2.14 vs 1.72 ms per configs[4] trace LDE, same box.)
 template <int LOGS>
 struct Plan {
     static constexpr int REM = LOGS % 4;
     static constexpr int NSTEP = LOGS / 4 + (REM ? 1 : 0);
     static constexpr int FIRST_LOGR = REM ? REM : 4;
     // radix of the step that produces the final outputs
-    static constexpr int LAST_R = NSTEP == 1 ? (1 << FIRST_LOGR) : 16;
+    static constexpr int LAST_LOGR = NSTEP == 1 ? FIRST_LOGR : 4;
+    static constexpr int LAST_R = 1 << LAST_LOGR;
 };
 
 // Whole DFT of every sequence: the first step loads with ldg (global), middle steps run in the
 // LDS tile, the last step stores with stg (global). A one-step DFT goes global -> global.
 // stg(q, seq, base, stride, v) stores group q's outputs; pf as in stockham, for the last step
-template <int LOGS, bool INV, bool FIRST_SEQ_FAST, class LDG, class STG, class PF>
+template <int LOGS, bool INV, bool FIRST_SEQ_FAST, int NT, class LDG, class STG, class PF>
 __device__ __forceinline__ void pass_dft(u64* tile, int lognseq, const u64* ltw, LDG ldg, STG stg, PF pf) {
     using PL = Plan<LOGS>;
     constexpr int PITCH = row_pitch(1 << LOGS);
     auto nopf = [](int, int, int, int) {};
     if constexpr (PL::NSTEP == 1) {
-        stockham<LOGS, PL::FIRST_LOGR, INV, FIRST_SEQ_FAST, false>(lognseq, 1, ltw, ldg, stg, pf);
+        stockham<LOGS, PL::FIRST_LOGR, INV, FIRST_SEQ_FAST, false, NT>(lognseq, 1, ltw, ldg, stg, pf);
     } else {
-        stockham<LOGS, PL::FIRST_LOGR, INV, FIRST_SEQ_FAST, false>(
+        stockham<LOGS, PL::FIRST_LOGR, INV, FIRST_SEQ_FAST, false, NT>(
             lognseq, 1, ltw, ldg, [&](int, int seq, int base, int stride, u64* v) {
                 u64* row = tile + seq * PITCH;
 #pragma unroll
@@ -228,7 +231,7 @@ __device__ __forceinline__ void pass_dft(u64* tile, int lognseq, const u64* ltw,
         int Ns = 1 << PL::FIRST_LOGR;
 #pragma unroll
         for (int st = 1; st < PL::NSTEP - 1; st++) {
-            stockham<LOGS, 4, INV, true, true>(
+            stockham<LOGS, 4, INV, true, true, NT>(
                 lognseq, Ns, ltw, [&](int seq, int i) { return tile[seq * PITCH + phys(i)]; },
                 [&](int, int seq, int base, int stride, u64* v) {
                     u64* row = tile + seq * PITCH;
@@ -239,8 +242,8 @@ __device__ __forceinline__ void pass_dft(u64* tile, int lognseq, const u64* ltw,
             __syncthreads();
             Ns <<= 4;
         }
-        stockham<LOGS, 4, INV, true, false>(lognseq, Ns, ltw,
-                                            [&](int seq, int i) { return tile[seq * PITCH + phys(i)]; }, stg, pf);
+        stockham<LOGS, PL::LAST_LOGR, INV, true, false, NT>(
+            lognseq, Ns, ltw, [&](int seq, int i) { return tile[seq * PITCH + phys(i)]; }, stg, pf);
         __syncthreads();
     }
 }
@@ -281,11 +284,13 @@ __device__ __forceinline__ void xcd_block(bool on, int& bx, int& by) {
 // forward, coset t: x[j1] = c[C j1 + j2] * 7^(C j1) w_(beta R)^(t j1)
 //   y[t][k1][j2] = X[k1] * 7^j2 * w_N^(j2 (t + beta k1))
 // inverse: y[k1][j2] = X[k1] * w_n^-(j2 k1)
-template <int LOGR, bool INV>
-__global__ __launch_bounds__(THREADS, 4) void ntt_pass_a(NttArgs a) {
-    constexpr int R = 1 << LOGR, PITCH = row_pitch(R), RR = Plan<LOGR>::LAST_R;
+// LOGT = log2 threads: 8 (4096-element tiles, several blocks per CU) or 10 (16384-element tiles
+// in up to 155 KiB of LDS, one block per CU: 16 columns per tile even at R = 1024)
+template <int LOGR, bool INV, int LOGT>
+__global__ __launch_bounds__(1 << LOGT, LOGT == 8 ? 4 : 1) void ntt_pass_a(NttArgs a) {
+    constexpr int R = 1 << LOGR, PITCH = row_pitch(R), RR = Plan<LOGR>::LAST_R, NT = 1 << LOGT;
     extern __shared__ u64 lds[];
-    const int logTC = (a.logC < 12 - LOGR) ? a.logC : 12 - LOGR;
+    const int logTC = (a.logC < LOGT + 4 - LOGR) ? a.logC : LOGT + 4 - LOGR;
     const int TC = 1 << logTC;
     u64* tile = lds;
     u64* ltw = lds + TC * PITCH;
@@ -298,7 +303,7 @@ __global__ __launch_bounds__(THREADS, 4) void ntt_pass_a(NttArgs a) {
     const u64 n = 1ULL << a.logn;
     const int logN = a.logn + a.logbeta;
     const u64 maskN = (1ULL << logN) - 1;
-    for (int i = threadIdx.x; i < R; i += THREADS) {
+    for (int i = threadIdx.x; i < R; i += NT) {
         ltw[i] = tw_get(a.T, LOGR, i, INV);
         if (!INV)
             pre[i] = gl_mul(a.T.pow7[(u64)i << a.logC],
@@ -343,15 +348,15 @@ __global__ __launch_bounds__(THREADS, 4) void ntt_pass_a(NttArgs a) {
             if (r + 1 < RR) w = gl_mul(w, step);
         }
     };
-    pass_dft<LOGR, INV, true>(tile, logTC, ltw, ldg, stg, pf);
+    pass_dft<LOGR, INV, true, NT>(tile, logTC, ltw, ldg, stg, pf);
 }
 
 // ---------------------------------------------------------------- pass B: row DFTs (size C)
-template <int LOGC, bool INV>
-__global__ __launch_bounds__(THREADS) void ntt_pass_b(NttArgs a) {
-    constexpr int C = 1 << LOGC, RR = Plan<LOGC>::LAST_R;
+template <int LOGC, bool INV, int LOGT>
+__global__ __launch_bounds__(1 << LOGT) void ntt_pass_b(NttArgs a) {
+    constexpr int C = 1 << LOGC, RR = Plan<LOGC>::LAST_R, NT = 1 << LOGT;
     extern __shared__ u64 lds[];
-    const int logTR = (a.logR < 12 - LOGC) ? a.logR : 12 - LOGC;
+    const int logTR = (a.logR < LOGT + 4 - LOGC) ? a.logR : LOGT + 4 - LOGC;
     const int TR = 1 << logTR;
     u64* tile = lds;
     u64* ltw = lds + TR * row_pitch(C);
@@ -359,7 +364,7 @@ __global__ __launch_bounds__(THREADS) void ntt_pass_b(NttArgs a) {
     xcd_block(a.xcd & 2, bx, by);
     const int pt = by, k10 = bx * TR;
     const u64 n = 1ULL << a.logn;
-    for (int i = threadIdx.x; i < C; i += THREADS) ltw[i] = tw_get(a.T, LOGC, i, INV);
+    for (int i = threadIdx.x; i < C; i += NT) ltw[i] = tw_get(a.T, LOGC, i, INV);
     __syncthreads();
     const u64* y = a.y + (u64)pt * n;
     auto ldg = [&](int seq, int j2) -> u64 { return y[((u64)(k10 + seq) << LOGC) + j2]; };
@@ -380,41 +385,64 @@ __global__ __launch_bounds__(THREADS) void ntt_pass_b(NttArgs a) {
     };
     // multi-step rows: first step along the row (coalesced loads); one-step rows: lanes along
     // sequences so the (final) global store is coalesced
-    pass_dft<LOGC, INV, (Plan<LOGC>::NSTEP == 1)>(tile, logTR, ltw, ldg, stg, [](int, int, int, int) {});
+    pass_dft<LOGC, INV, (Plan<LOGC>::NSTEP == 1), NT>(tile, logTR, ltw, ldg, stg, [](int, int, int, int) {});
 }
 
 // ---------------------------------------------------------------- dispatch
+// tiles above 64 KiB of LDS need the per-kernel opt-in (a workgroup may use 160 KiB on gfx950)
+#define XFG_NTT_LAUNCH(KERNEL, NT)                                                                          \
+    do {                                                                                                    \
+        if (lds > 65536) {                                                                                  \
+            static const bool ok_ = hipFuncSetAttribute((const void*)KERNEL,                                \
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize,         \
+                                                        160 * 1024) == hipSuccess;                          \
+            (void)ok_;                                                                                      \
+        }                                                                                                   \
+        hipLaunchKernelGGL(KERNEL, g, dim3(NT), lds, s, a);                                                 \
+    } while (0)
 template <bool INV>
-static void run_pass_a(int logR, dim3 g, size_t lds, hipStream_t s, const NttArgs& a) {
+static void run_pass_a(int logR, int logT, dim3 g, size_t lds, hipStream_t s, const NttArgs& a) {
 #define XFG_CASE_A(L) \
-    case L: hipLaunchKernelGGL((ntt_pass_a<L, INV>), g, dim3(THREADS), lds, s, a); break;
+    case L: XFG_NTT_LAUNCH((ntt_pass_a<L, INV, 8>), 256); break;
+#define XFG_CASE_A10(L) \
+    case L: XFG_NTT_LAUNCH((ntt_pass_a<L, INV, 10>), 1024); break;
+    if (logT == 10) {
+        switch (logR) {
+            XFG_CASE_A10(9) XFG_CASE_A10(10)
+            default: break;
+        }
+        return;
+    }
     switch (logR) {
         XFG_CASE_A(1) XFG_CASE_A(2) XFG_CASE_A(3) XFG_CASE_A(4) XFG_CASE_A(5) XFG_CASE_A(6)
         XFG_CASE_A(7) XFG_CASE_A(8) XFG_CASE_A(9) XFG_CASE_A(10)
         default: break;
     }
 #undef XFG_CASE_A
+#undef XFG_CASE_A10
 }
 template <bool INV>
-static void run_pass_b(int logC, dim3 g, size_t lds, hipStream_t s, const NttArgs& a) {
-    // C = 4096 rows need 67 KiB of LDS (a workgroup may use up to 160 KiB on gfx950)
-#define XFG_CASE_B(L)                                                                                         \
-    case L:                                                                                                   \
-        if (lds > 65536) {                                                                                    \
-            static const bool ok_ = hipFuncSetAttribute((const void*)ntt_pass_b<L, INV>,                      \
-                                                        hipFuncAttributeMaxDynamicSharedMemorySize,           \
-                                                        160 * 1024) == hipSuccess;                            \
-            (void)ok_;                                                                                        \
-        }                                                                                                     \
-        hipLaunchKernelGGL((ntt_pass_b<L, INV>), g, dim3(THREADS), lds, s, a);                                \
-        break;
+static void run_pass_b(int logC, int logT, dim3 g, size_t lds, hipStream_t s, const NttArgs& a) {
+#define XFG_CASE_B(L) \
+    case L: XFG_NTT_LAUNCH((ntt_pass_b<L, INV, 8>), 256); break;
+#define XFG_CASE_B10(L) \
+    case L: XFG_NTT_LAUNCH((ntt_pass_b<L, INV, 10>), 1024); break;
+    if (logT == 10) {
+        switch (logC) {
+            XFG_CASE_B10(9) XFG_CASE_B10(10) XFG_CASE_B10(11)
+            default: break;
+        }
+        return;
+    }
     switch (logC) {
         XFG_CASE_B(2) XFG_CASE_B(3) XFG_CASE_B(4) XFG_CASE_B(5) XFG_CASE_B(6) XFG_CASE_B(7)
         XFG_CASE_B(8) XFG_CASE_B(9) XFG_CASE_B(10) XFG_CASE_B(11) XFG_CASE_B(12)
         default: break;
     }
 #undef XFG_CASE_B
+#undef XFG_CASE_B10
 }
+#undef XFG_NTT_LAUNCH
 
 // split n = R * C: evenly below 2^18, C = 2R from 2^18 on (faster at 2^18 and 2^20, see
 // scripts/ntt_split.py); XFG_NTT_LOGC forces log2(C) for tuning sweeps
@@ -459,8 +487,17 @@ void build_fourstep(u64* out, int logn, int logbeta, const Tables& T, hipStream_
 static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
     ntt_split(a.logn, a.logR, a.logC);
     const int R = 1 << a.logR, C = 1 << a.logC;
-    const int logTC = a.logC < 12 - a.logR ? a.logC : 12 - a.logR;
-    const int logTR = a.logR < 12 - a.logC ? a.logR : 12 - a.logC;
+    // wide tiles (1024 threads, 16384 elements) where a 4096-element tile would hold fewer than 16
+    // columns (pass A, R >= 512) or rows (pass B, C >= 512): the scattered stores then write whole
+    // 128 B lines (XFG_NTT_WIDE=0 disables, for A/B runs)
+    static const bool wide_on = [] {
+        const char* v = getenv("XFG_NTT_WIDE");
+        return !(v && *v == '0');
+    }();
+    const int ltA = (wide_on && a.logR >= 9 && a.logR <= 10 && a.logC >= 4) ? 10 : 8;
+    const int ltB = (wide_on && a.logC >= 9 && a.logC <= 11 && a.logR >= 4) ? 10 : 8;
+    const int logTC = a.logC < ltA + 4 - a.logR ? a.logC : ltA + 4 - a.logR;
+    const int logTR = a.logR < ltB + 4 - a.logC ? a.logR : ltB + 4 - a.logC;
     const int ncos = inv ? 1 : (1 << a.logbeta);
     size_t lds_a = ((size_t)(1 << logTC) * row_pitch(R) + 2 * R) * sizeof(u64);
     size_t lds_b = ((size_t)(1 << logTR) * row_pitch(C) + C) * sizeof(u64);
@@ -473,11 +510,11 @@ static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
     }();
     a.xcd = xcd_on ? ((logTC < 4 ? 1 : 0) | (logTR < 4 ? 2 : 0)) : 0;
     if (inv) {
-        run_pass_a<true>(a.logR, ga, lds_a, s, a);
-        run_pass_b<true>(a.logC, gb, lds_b, s, a);
+        run_pass_a<true>(a.logR, ltA, ga, lds_a, s, a);
+        run_pass_b<true>(a.logC, ltB, gb, lds_b, s, a);
     } else {
-        run_pass_a<false>(a.logR, ga, lds_a, s, a);
-        run_pass_b<false>(a.logC, gb, lds_b, s, a);
+        run_pass_a<false>(a.logR, ltA, ga, lds_a, s, a);
+        run_pass_b<false>(a.logC, ltB, gb, lds_b, s, a);
     }
 }
 
