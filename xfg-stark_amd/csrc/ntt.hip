@@ -287,7 +287,7 @@ __device__ __forceinline__ void xcd_block(bool on, int& bx, int& by) {
 // LOGT = log2 threads: 8 (4096-element tiles, several blocks per CU) or 10 (16384-element tiles
 // in up to 155 KiB of LDS, one block per CU: 16 columns per tile even at R = 1024)
 template <int LOGR, bool INV, int LOGT>
-__global__ __launch_bounds__(1 << LOGT, LOGT == 8 ? 4 : 1) void ntt_pass_a(NttArgs a) {
+__global__ __launch_bounds__(1 << LOGT, 1 << (10 - LOGT)) void ntt_pass_a(NttArgs a) {
     constexpr int R = 1 << LOGR, PITCH = row_pitch(R), RR = Plan<LOGR>::LAST_R, NT = 1 << LOGT;
     extern __shared__ u64 lds[];
     const int logTC = (a.logC < LOGT + 4 - LOGR) ? a.logC : LOGT + 4 - LOGR;
@@ -406,9 +406,18 @@ static void run_pass_a(int logR, int logT, dim3 g, size_t lds, hipStream_t s, co
     case L: XFG_NTT_LAUNCH((ntt_pass_a<L, INV, 8>), 256); break;
 #define XFG_CASE_A10(L) \
     case L: XFG_NTT_LAUNCH((ntt_pass_a<L, INV, 10>), 1024); break;
+#define XFG_CASE_A9(L) \
+    case L: XFG_NTT_LAUNCH((ntt_pass_a<L, INV, 9>), 512); break;
     if (logT == 10) {
         switch (logR) {
             XFG_CASE_A10(9) XFG_CASE_A10(10)
+            default: break;
+        }
+        return;
+    }
+    if (logT == 9) {
+        switch (logR) {
+            XFG_CASE_A9(9) XFG_CASE_A9(10)
             default: break;
         }
         return;
@@ -420,6 +429,7 @@ static void run_pass_a(int logR, int logT, dim3 g, size_t lds, hipStream_t s, co
     }
 #undef XFG_CASE_A
 #undef XFG_CASE_A10
+#undef XFG_CASE_A9
 }
 template <bool INV>
 static void run_pass_b(int logC, int logT, dim3 g, size_t lds, hipStream_t s, const NttArgs& a) {
@@ -427,9 +437,18 @@ static void run_pass_b(int logC, int logT, dim3 g, size_t lds, hipStream_t s, co
     case L: XFG_NTT_LAUNCH((ntt_pass_b<L, INV, 8>), 256); break;
 #define XFG_CASE_B10(L) \
     case L: XFG_NTT_LAUNCH((ntt_pass_b<L, INV, 10>), 1024); break;
+#define XFG_CASE_B9(L) \
+    case L: XFG_NTT_LAUNCH((ntt_pass_b<L, INV, 9>), 512); break;
     if (logT == 10) {
         switch (logC) {
             XFG_CASE_B10(9) XFG_CASE_B10(10) XFG_CASE_B10(11)
+            default: break;
+        }
+        return;
+    }
+    if (logT == 9) {
+        switch (logC) {
+            XFG_CASE_B9(9) XFG_CASE_B9(10) XFG_CASE_B9(11)
             default: break;
         }
         return;
@@ -441,6 +460,7 @@ static void run_pass_b(int logC, int logT, dim3 g, size_t lds, hipStream_t s, co
     }
 #undef XFG_CASE_B
 #undef XFG_CASE_B10
+#undef XFG_CASE_B9
 }
 #undef XFG_NTT_LAUNCH
 
@@ -494,8 +514,20 @@ static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
         const char* v = getenv("XFG_NTT_WIDE");
         return !(v && *v == '0');
     }();
-    const int ltA = (wide_on && a.logR >= 9 && a.logR <= 10 && a.logC >= 4) ? 10 : 8;
-    const int ltB = (wide_on && a.logC >= 9 && a.logC <= 11 && a.logR >= 4) ? 10 : 8;
+    // XFG_NTT_LTA / XFG_NTT_LTB force log2(threads) 8, 9 or 10 of the wide-capable passes (sweeps)
+    static const int force_lta = [] {
+        const char* v = getenv("XFG_NTT_LTA");
+        return v && *v ? atoi(v) : 0;
+    }();
+    static const int force_ltb = [] {
+        const char* v = getenv("XFG_NTT_LTB");
+        return v && *v ? atoi(v) : 0;
+    }();
+    const bool capA = a.logR >= 9 && a.logR <= 10 && a.logC >= 4, capB = a.logC >= 9 && a.logC <= 11 && a.logR >= 4;
+    const int ltA = capA ? (force_lta >= 8 && force_lta <= 10 ? force_lta : (wide_on ? 10 : 8)) : 8;
+    // pass B: 512 threads (8192 elements, <= 78 KiB, two blocks per CU) up to C = 1024 -- the second
+    // block hides the first one's barriers and load latency; 1024 threads at C = 2048
+    const int ltB = capB ? (force_ltb >= 8 && force_ltb <= 10 ? force_ltb : (wide_on ? (a.logC <= 10 ? 9 : 10) : 8)) : 8;
     const int logTC = a.logC < ltA + 4 - a.logR ? a.logC : ltA + 4 - a.logR;
     const int logTR = a.logR < ltB + 4 - a.logC ? a.logR : ltB + 4 - a.logC;
     const int ncos = inv ? 1 : (1 << a.logbeta);
