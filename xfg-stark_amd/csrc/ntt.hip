@@ -100,6 +100,23 @@ __device__ __forceinline__ u64 add_w(u64 a, u64 b) {  // b < p
 __device__ __forceinline__ u64 sub_w(u64 a, u64 b) { return gl_sub_weak(a, b); }  // b < p
 __device__ __forceinline__ u64 canon(u64 x) { return gl_canon(x); }
 
+// Raw buffer access for the passes' strided global loads / stores: the per-lane part of an address
+// is a 32-bit VGPR offset computed once per group, the part that varies with the butterfly output
+// r (r * stride rows) is wave-uniform and goes in the SGPR offset -- no 64-bit address arithmetic
+// on the VALU per element. Bases are per (poly, coset) planes, so offsets stay below 2^32 bytes.
+typedef u32 u32x2 __attribute__((__vector_size__(8)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const u64* p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<u64*>(p), (short)0, -1, 0x00020000);
+}
+__device__ __forceinline__ u64 buf_ld(__amdgpu_buffer_rsrc_t r, u32 voff, u32 soff) {
+    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, 0);
+    return (u64)v[0] | ((u64)v[1] << 32);
+}
+__device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, u32 voff, u32 soff, u64 x) {
+    const u32x2 v = {(u32)x, (u32)(x >> 32)};
+    __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)voff, (int)soff, 0);
+}
+
 // in-register DFT of size 2^LOGR (<= 16): v[q] <- sum_r v[r] w_R^(+-rq), natural order in/out.
 // In: v[r] < p for every r whose bit-reversed position is odd (the level-0 subtrahends: every
 // r >= R/2), the rest may be weak. Out: weak. The shift multiplies return canonical values, so
@@ -153,7 +170,8 @@ __device__ __forceinline__ u64 tw_get(const Tables& T, int k, u64 e, bool inv) {
 // ---------------------------------------------------------------- one Stockham step
 // Radix 2^LOGR step of a size-2^LOGS DFT on 2^lognseq sequences. Group g of the step is
 // (seq, j); SEQ_FAST maps consecutive lanes to consecutive sequences, otherwise to consecutive j.
-// ld(seq, i) reads logical element i of a sequence; st(seq, base, stride, v) receives the R
+// ld(seq, j, o) reads logical element i = j + o of a sequence (o = r * G, uniform across the
+// wave); st(seq, base, stride, v) receives the R
 // outputs of a group, which belong at logical positions base + r * stride.
 // IN_PLACE: every load of the step completes (barrier) before any store.
 // pf(q, seq, base, stride) runs before the group's loads (prefetch of what st will need).
@@ -174,7 +192,7 @@ __device__ __forceinline__ void stockham(int lognseq, int Ns, const u64* ltw, LD
             const int j = SEQ_FAST ? (g >> lognseq) : (g % G);
             pf(q, seq, (j / Ns) * Ns * R + (j % Ns), Ns);
 #pragma unroll
-            for (int r = 0; r < R; r++) v[q][r] = ld(seq, j + r * G);
+            for (int r = 0; r < R; r++) v[q][r] = ld(seq, j, r * G);
             if (Ns > 1) {
                 const int k = j % Ns, step = S / (Ns * R);
 #pragma unroll
@@ -232,7 +250,7 @@ __device__ __forceinline__ void pass_dft(u64* tile, int lognseq, const u64* ltw,
 #pragma unroll
         for (int st = 1; st < PL::NSTEP - 1; st++) {
             stockham<LOGS, 4, INV, true, true, NT>(
-                lognseq, Ns, ltw, [&](int seq, int i) { return tile[seq * PITCH + phys(i)]; },
+                lognseq, Ns, ltw, [&](int seq, int j, int o) { return tile[seq * PITCH + phys(j + o)]; },
                 [&](int, int seq, int base, int stride, u64* v) {
                     u64* row = tile + seq * PITCH;
 #pragma unroll
@@ -243,7 +261,7 @@ __device__ __forceinline__ void pass_dft(u64* tile, int lognseq, const u64* ltw,
             Ns <<= 4;
         }
         stockham<LOGS, PL::LAST_LOGR, INV, true, false, NT>(
-            lognseq, Ns, ltw, [&](int seq, int i) { return tile[seq * PITCH + phys(i)]; }, stg, pf);
+            lognseq, Ns, ltw, [&](int seq, int j, int o) { return tile[seq * PITCH + phys(j + o)]; }, stg, pf);
         __syncthreads();
     }
 }
@@ -312,25 +330,29 @@ __global__ __launch_bounds__(1 << LOGT, 1 << (10 - LOGT)) void ntt_pass_a(NttArg
     __syncthreads();
     const u64* in = a.in + (u64)poly * a.in_stride;
     u64* y = a.y + (u64)pt * n;
-    auto ldg = [&](int seq, int j1) -> u64 {
-        u64 v = in[((u64)j1 << a.logC) + col0 + seq];
-        return INV ? v : gl_mul(v, pre[j1]);
+    const auto rin = buf_rsrc(in + col0), ry = buf_rsrc(y + col0);
+    auto ldg = [&](int seq, int j, int o) -> u64 {
+        const u64 v = buf_ld(rin, (((u32)j << a.logC) + seq) * 8, ((u32)o << a.logC) * 8);
+        return INV ? v : gl_mul(v, pre[j + o]);
     };
     // four-step twiddles from the table: loaded by pf before the last step's loads and butterflies,
     // so the table latency hides behind them; one multiply per element instead of two
     constexpr int PERL = 16 / RR;
     u64 tq[PERL][RR];
     const u64* tab = a.t4 ? a.t4 + (INV ? 0 : ((u64)t << a.logn)) + col0 : nullptr;
+    const auto rtab = buf_rsrc(tab ? tab : y);
     auto pf = [&](int q, int seq, int base, int stride) {
         if (!tab) return;
+        const u32 vo = (((u32)base << a.logC) + seq) * 8;
 #pragma unroll
-        for (int r = 0; r < RR; r++) tq[q][r] = tab[((u64)(base + r * stride) << a.logC) + seq];
+        for (int r = 0; r < RR; r++) tq[q][r] = buf_ld(rtab, vo, ((u32)(r * stride) << a.logC) * 8);
     };
     auto stg = [&](int q, int seq, int base, int stride, u64* v) {
         const u64 j2 = col0 + seq;
         if (tab) {
+            const u32 vo = (((u32)base << a.logC) + seq) * 8;
 #pragma unroll
-            for (int r = 0; r < RR; r++) y[((u64)(base + r * stride) << a.logC) + j2] = gl_mul(v[r], tq[q][r]);
+            for (int r = 0; r < RR; r++) buf_st(ry, vo, ((u32)(r * stride) << a.logC) * 8, gl_mul(v[r], tq[q][r]));
             return;
         }
         u64 w, step;
@@ -367,7 +389,8 @@ __global__ __launch_bounds__(1 << LOGT) void ntt_pass_b(NttArgs a) {
     for (int i = threadIdx.x; i < C; i += NT) ltw[i] = tw_get(a.T, LOGC, i, INV);
     __syncthreads();
     const u64* y = a.y + (u64)pt * n;
-    auto ldg = [&](int seq, int j2) -> u64 { return y[((u64)(k10 + seq) << LOGC) + j2]; };
+    auto ldg = [&](int seq, int j, int o) -> u64 { return y[((u64)(k10 + seq) << LOGC) + j + o]; };
+    const auto rout = buf_rsrc(a.out + (u64)pt * n + k10);
     auto stg = [&](int, int seq, int base, int stride, u64* v) {
 #pragma unroll
         for (int r = 0; r < RR; r++) {
@@ -379,7 +402,8 @@ __global__ __launch_bounds__(1 << LOGT) void ntt_pass_b(NttArgs a) {
                     a.out[(u64)pt * a.out_stride + k] = x;
                 }
             } else {
-                a.out[(u64)pt * n + k] = canon(v[r]);  // pt = poly * beta + t -> coset-major
+                // pt = poly * beta + t -> coset-major; k - k10 = seq + (base + r stride) R
+                buf_st(rout, (seq + ((u32)base << a.logR)) * 8, ((u32)(r * stride) << a.logR) * 8, canon(v[r]));
             }
         }
     };
