@@ -159,6 +159,10 @@ __device__ __forceinline__ void dft_reg(u64* v) {
 // for lanes walking across rows.
 __host__ __device__ constexpr int row_pitch(int S) { return S + S / 16 + 1; }
 __device__ __forceinline__ int phys(int i) { return i + (i >> 4); }
+// phys(j + o) for an offset o that is a compile-time constant after unrolling: a multiple of 16
+// splits off as a constant (the LDS instruction's immediate offset), so the per-lane index
+// phys(j) is computed once per group instead of once per element
+__device__ __forceinline__ int phys2(int j, int o) { return (o & 15) == 0 ? phys(j) + o + (o >> 4) : phys(j + o); }
 
 __device__ __forceinline__ u64 tw_get(const Tables& T, int k, u64 e, bool inv) {
     const u64 M = 1ULL << T.LM;
@@ -242,7 +246,11 @@ __device__ __forceinline__ void pass_dft(u64* tile, int lognseq, const u64* ltw,
             lognseq, 1, ltw, ldg, [&](int, int seq, int base, int stride, u64* v) {
                 u64* row = tile + seq * PITCH;
 #pragma unroll
-                for (int r = 0; r < (1 << PL::FIRST_LOGR); r++) row[phys(base + r * stride)] = v[r];
+                for (int r = 0; r < (1 << PL::FIRST_LOGR); r++) {
+                    // radix-16 first step: base = 16 j, stride 1 -> the 16 outputs are contiguous
+                    if constexpr (PL::FIRST_LOGR == 4) row[phys(base) + r] = v[r];
+                    else row[phys(base + r * stride)] = v[r];
+                }
             },
             nopf);
         __syncthreads();
@@ -250,18 +258,18 @@ __device__ __forceinline__ void pass_dft(u64* tile, int lognseq, const u64* ltw,
 #pragma unroll
         for (int st = 1; st < PL::NSTEP - 1; st++) {
             stockham<LOGS, 4, INV, true, true, NT>(
-                lognseq, Ns, ltw, [&](int seq, int j, int o) { return tile[seq * PITCH + phys(j + o)]; },
+                lognseq, Ns, ltw, [&](int seq, int j, int o) { return tile[seq * PITCH + phys2(j, o)]; },
                 [&](int, int seq, int base, int stride, u64* v) {
                     u64* row = tile + seq * PITCH;
 #pragma unroll
-                    for (int r = 0; r < 16; r++) row[phys(base + r * stride)] = v[r];
+                    for (int r = 0; r < 16; r++) row[phys2(base, r * stride)] = v[r];
                 },
                 nopf);
             __syncthreads();
             Ns <<= 4;
         }
         stockham<LOGS, PL::LAST_LOGR, INV, true, false, NT>(
-            lognseq, Ns, ltw, [&](int seq, int j, int o) { return tile[seq * PITCH + phys(j + o)]; }, stg, pf);
+            lognseq, Ns, ltw, [&](int seq, int j, int o) { return tile[seq * PITCH + phys2(j, o)]; }, stg, pf);
         __syncthreads();
     }
 }
