@@ -188,24 +188,22 @@ __device__ __forceinline__ void stockham(int lognseq, int Ns, const u64* ltw, LD
     int gs[PER], gj[PER];
 #pragma unroll
     for (int q = 0; q < PER; q++) {
-        const int g = threadIdx.x + NT * q;
-        gs[q] = -1;
-        gj[q] = 0;
-        if (g < groups) {
-            const int seq = SEQ_FAST ? (g & (nseq - 1)) : (g / G);
-            const int j = SEQ_FAST ? (g >> lognseq) : (g % G);
-            pf(q, seq, (j / Ns) * Ns * R + (j % Ns), Ns);
+        // lanes past the last group (partial tiles only) recompute the last group and drop the
+        // result: no divergent branch, and no zero-initialised registers for the untaken path
+        const int g0 = threadIdx.x + NT * q, g = g0 < groups ? g0 : groups - 1;
+        const int seq = SEQ_FAST ? (g & (nseq - 1)) : (g / G);
+        const int j = SEQ_FAST ? (g >> lognseq) : (g % G);
+        pf(q, seq, (j / Ns) * Ns * R + (j % Ns), Ns);
 #pragma unroll
-            for (int r = 0; r < R; r++) v[q][r] = ld(seq, j, r * G);
-            if (Ns > 1) {
-                const int k = j % Ns, step = S / (Ns * R);
+        for (int r = 0; r < R; r++) v[q][r] = ld(seq, j, r * G);
+        if (Ns > 1) {
+            const int k = j % Ns, step = S / (Ns * R);
 #pragma unroll
-                for (int r = 1; r < R; r++) v[q][r] = gl_mul(v[q][r], ltw[r * k * step]);
-            }
-            dft_reg<LOGR, INV>(v[q]);
-            gs[q] = seq;
-            gj[q] = j;
+            for (int r = 1; r < R; r++) v[q][r] = gl_mul(v[q][r], ltw[r * k * step]);
         }
+        dft_reg<LOGR, INV>(v[q]);
+        gs[q] = g0 < groups ? seq : -1;
+        gj[q] = j;
     }
     if (IN_PLACE) __syncthreads();
 #pragma unroll
