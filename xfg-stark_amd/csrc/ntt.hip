@@ -105,8 +105,14 @@ __device__ __forceinline__ u64 canon(u64 x) { return gl_canon(x); }
 // r (r * stride rows) is wave-uniform and goes in the SGPR offset -- no 64-bit address arithmetic
 // on the VALU per element. Bases are per (poly, coset) planes, so offsets stay below 2^32 bytes.
 typedef u32 u32x2 __attribute__((__vector_size__(8)));
+// p must be wave-uniform; it is read from the first lane so that the descriptor is built in SGPRs
+// (a descriptor the compiler cannot prove uniform gets a readfirstlane/compare loop around every
+// access)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const u64* p) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<u64*>(p), (short)0, -1, 0x00020000);
+    const u64 a = (u64)p;
+    const u64 u = (u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)a) |
+                  ((u64)(u32)__builtin_amdgcn_readfirstlane((int)(u32)(a >> 32)) << 32);
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(u), (short)0, -1, 0x00020000);
 }
 __device__ __forceinline__ u64 buf_ld(__amdgpu_buffer_rsrc_t r, u32 voff, u32 soff) {
     const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, 0);
