@@ -68,17 +68,17 @@ def _field_inputs(canonical, seed):
     return a, b
 
 
-@pytest.mark.parametrize("op", ["mul", "add", "sub", "canon", "pow2", "fold", "sub_weak"])
+@pytest.mark.parametrize("op", ["mul", "add", "sub", "canon", "pow2", "fold", "sub_weak", "add_w"])
 def test_field_primitives_match_bigint(prover, op):
     """the gfx950 inline-asm Goldilocks primitives (gl.hpp) against Python integers, edge values
     (0, 2^32 - 1, p - 1, p, 2^64 - 1, ...) crossed with each other plus random operands"""
     canonical_in = op in ("add", "sub")
-    a, b = _field_inputs(canonical_in, hash(op) & 0xFFFF)
+    a, b = _field_inputs(canonical_in, sum(op.encode()))
     if op == "pow2":
         b = [y % 96 for y in b]
     if op == "fold":
         b = [y & 0xFFFFFFFF for y in b]
-    if op == "sub_weak":  # butterfly contract: subtrahend < p
+    if op in ("sub_weak", "add_w"):  # butterfly contract: subtrahend / addend < p
         b = [y % P_GL for y in b]
     got = prover.debug_field(op, np.array(a, dtype=np.uint64), np.array(b, dtype=np.uint64)).tolist()
     for x, y, r in zip(a, b, got):
@@ -97,6 +97,11 @@ def test_field_primitives_match_bigint(prover, op):
                 continue
         elif op == "fold":
             want = (x + y * 0xFFFFFFFF) % P_GL
+        elif op == "add_w":  # weak: the 64-bit sum with one carry folded in as + (2^32 - 1)
+            want = x + y if x + y < (1 << 64) else x + y - (1 << 64) + 0xFFFFFFFF
+            assert want < (1 << 64) and want % P_GL == (x + y) % P_GL
+            assert r == want, (op, x, y, r, want)
+            continue
         else:
             want = x - y if x >= y else x - y + P_GL
             assert r == want, (op, x, y, r, want)

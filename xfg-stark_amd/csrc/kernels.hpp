@@ -50,7 +50,7 @@ void launch_lde(const u64* coef, u64 coef_stride, u64* out, u64* scratch, int np
 u64 fourstep_size(int logn, int logbeta);
 void build_fourstep(u64* out, int logn, int logbeta, const Tables& T, hipStream_t s);
 // field-primitive self test (xfg_debug_field): op 0 mul, 1 add, 2 sub, 3 canon(a), 4 a * 2^b,
-// 5 fold(a, (u32)b), 6 sub_weak(a, b)
+// 5 fold(a, (u32)b), 6 sub_weak(a, b), 7 add_w(a, b) (the NTT butterfly add, b < p)
 void launch_field_op(int op, const u64* a, const u64* b, u64* out, u64 count, hipStream_t s);
 // inverse: evals[poly][n] at 7^off7 * w_n^i -> coefficients (first `keep` written, stride out_stride)
 void launch_interpolate(const u64* evals, u64 in_stride, u64* out, u64 out_stride, u64* scratch, int npoly, int logn,

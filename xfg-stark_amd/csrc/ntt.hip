@@ -83,19 +83,21 @@ __host__ __device__ constexpr int brev_c(int x, int bits) {
 // Weakly reduced values: any u64 congruent mod p. The butterflies keep their outputs weak and
 // reduce only the subtrahend / addend t (which must be < p for these forms): u + t carries at most
 // once past 2^64 when t < p, and u - t borrows into a value >= EPS when t < p.
-// u + t as s = u + t plus (carry) EPS via one v_mad_u64_u32 (4 VALU; the compiler's form built a
-// {mask, 0} register pair with a v_mov for every add)
+// u + t as s = u + t plus (carry) EPS. The carry out of bit 63 is bit 31 of
+// (a_hi & b_hi) | ((a_hi | b_hi) & ~s_hi): one full-rate v_bitop3_b32 (truth table 0xd4 over
+// src0, src1, src2 = a_hi, b_hi, s_hi) and one full-rate shift, then one v_mad_u64_u32 adds
+// carry * EPS -- 2 half-rate + 2 full-rate instructions and no VALU -> SGPR -> VALU mask hand-off
+// (the compare / cndmask form was 4 half-rate instructions plus an s_nop). No second carry: with
+// t < p, s = u + t - 2^64 <= p - 2 and s + EPS < 2^64.
 __device__ __forceinline__ u64 add_w(u64 a, u64 b) {  // b < p
-    u64 s, out, c;
-    u32 sel;
-    asm("v_lshl_add_u64 %[s], %[a], 0, %[b]\n\t"
-        "v_cmp_lt_u64_e64 %[c], %[s], %[b]\n\t"
-        "s_nop 1\n\t"
-        "v_cndmask_b32_e64 %[sel], 0, 1, %[c]\n\t"
-        "v_mad_u64_u32 %[out], %[c], %[sel], -1, %[s]"
-        : [s] "=&v"(s), [out] "=&v"(out), [sel] "=&v"(sel), [c] "=&s"(c)
-        : [a] "v"(a), [b] "v"(b));
-    return out;
+    u64 s;
+    u32 c;
+    asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(s) : "v"(a), "v"(b));
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xd4\n\t"
+        "v_lshrrev_b32 %0, 31, %0"
+        : "=&v"(c)
+        : "v"((u32)(a >> 32)), "v"((u32)(b >> 32)), "v"((u32)(s >> 32)));
+    return s + (u64)c * EPS;
 }
 __device__ __forceinline__ u64 sub_w(u64 a, u64 b) { return gl_sub_weak(a, b); }  // b < p
 __device__ __forceinline__ u64 canon(u64 x) { return gl_canon(x); }
@@ -654,6 +656,7 @@ __global__ void field_op_kernel(int op, const u64* a, const u64* b, u64* out, u6
         }
         case 5: r = gl_fold(x, (u32)y); break;
         case 6: r = gl_sub_weak(x, y); break;
+        case 7: r = add_w(x, y); break;
         default: break;
     }
     out[i] = r;
