@@ -143,3 +143,20 @@ def evaluate_lde(coef, blowup, offset=7):
     out = (C.c_uint64 * (n * blowup))()
     lib().orc_evaluate_lde(cb, n, blowup, offset, out)
     return list(out)
+
+
+def evaluate_lde_np(coef, blowup, offset=7):
+    """evaluate_lde over numpy uint64 arrays (no Python-int lists: for the 2^20+ parity cases)"""
+    import numpy as np
+    cb = np.ascontiguousarray(coef, dtype=np.uint64)
+    out = np.zeros(cb.size * blowup, dtype=np.uint64)
+    lib().orc_evaluate_lde(cb.ctypes.data_as(C.POINTER(C.c_uint64)), cb.size, blowup, offset,
+                           out.ctypes.data_as(C.POINTER(C.c_uint64)))
+    return out
+
+
+def interpolate_np(vals, offset=1):
+    import numpy as np
+    buf = np.array(vals, dtype=np.uint64, copy=True)
+    lib().orc_interpolate(buf.ctypes.data_as(C.POINTER(C.c_uint64)), buf.size, offset)
+    return buf

@@ -55,6 +55,25 @@ def test_lde_kernel_matches_oracle(prover, n, blowup):
         assert [int(v) for v in got[p]] == want
 
 
+@pytest.mark.parametrize("n,blowup", [(1 << 18, 2), (1 << 22, 2)])
+def test_lde_kernel_tile_paths_match_oracle(prover, n, blowup):
+    """the remaining four-step shapes: 2^18 (R = 256 narrow tiles, C = 1024 with 512-thread pass B
+    tiles) and 2^22 (R = 1024 wide 1024-thread pass A, C = 4096 narrow pass B), one polynomial,
+    compared as arrays"""
+    rng = np.random.default_rng(n + 7)
+    coef = rng.integers(0, P, size=(1, n), dtype=np.uint64)
+    got = np.asarray(prover.debug_lde(coef, n, blowup))[0]
+    assert np.array_equal(got, O.evaluate_lde_np(coef[0], blowup, 7))
+
+
+@pytest.mark.parametrize("n,off7", [(1 << 18, True), (1 << 22, False)])
+def test_interpolate_kernel_tile_paths_match_oracle(prover, n, off7):
+    rng = np.random.default_rng(n + 11)
+    ev = rng.integers(0, P, size=(1, n), dtype=np.uint64)
+    got = np.asarray(prover.debug_interpolate(ev, n, off7))[0]
+    assert np.array_equal(got, O.interpolate_np(ev[0], 7 if off7 else 1))
+
+
 P_GL = (1 << 64) - (1 << 32) + 1
 _EDGE = [0, 1, 2, 3, (1 << 32) - 1, 1 << 32, (1 << 32) + 1, (1 << 63) - 1, 1 << 63, P_GL - 2, P_GL - 1,
          P_GL, P_GL + 1, (1 << 64) - 2, (1 << 64) - 1, 0xFFFFFFFF00000000, 0x00000000FFFFFFFE]

@@ -109,6 +109,10 @@ def test_ntt_roundtrip_and_lde_definition():
     # interpolation over the coset recovers the coefficients (zero-padded)
     back = O.interpolate(lde, 7)
     assert back[:n] == coef and all(v == 0 for v in back[n:])
+    # the numpy-array wrappers the large GPU parity cases use agree with the list forms
+    import numpy as np
+    assert O.evaluate_lde_np(np.array(coef, dtype=np.uint64), beta, 7).tolist() == lde
+    assert O.interpolate_np(np.array(lde, dtype=np.uint64), 7).tolist() == back
 
 
 @pytest.mark.parametrize("case", [c for c in load("proofs.json") if c["n"] <= 4096], ids=lambda c: c["name"])
