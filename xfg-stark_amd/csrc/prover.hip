@@ -1030,7 +1030,7 @@ struct Batch {
 };
 
 static int max_lanes() {
-    static const int v = std::max(1, env_int("XFG_LANES", 5));
+    static const int v = std::max(1, env_int("XFG_LANES", 7));
     return v;
 }
 static int unit_size() {
