@@ -127,11 +127,11 @@ typedef struct {
     xfg_options options;
     uint32_t num_unique_queries;
     uint32_t num_fri_layers;
-    uint32_t remainder_len;     /* FRI remainder coefficients */
+    uint32_t remainder_len;     /* FRI remainder coefficients (E elements, not coordinates) */
     uint64_t pow_nonce;
     uint8_t trace_root[32];
     uint8_t constraint_root[32];
-    uint64_t ood_trace[14];     /* T_c(z), T_c(z g) interleaved */
+    uint64_t ood_trace[14];     /* T_c(z), T_c(z g) interleaved (first coordinates with an extension) */
     uint64_t ood_composition;   /* H(z) */
     size_t size;                /* bytes consumed == len for a well-formed proof */
 } xfg_proof_info;

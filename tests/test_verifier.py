@@ -115,6 +115,75 @@ def test_from_bytes_rejects_malformed(X):
         with pytest.raises(X.XfgStarkError) as e:
             X.StarkProof.from_bytes(bad)
         assert e.value.status == 10 and "ProofDeserializationError" in str(e.value)
+    # OOD frames with fewer (or more) values than 2 rows x 7 columns: rejected by the parser
+    # before anything reads the 14 values (an empty frame used to be read past the end)
+    sec = _sections(data)
+    at, ln = sec["ood"]
+    for k in (0, 2, 13, 15):
+        frame = (data[at:at + ln] * 2)[:8 * k]
+        bad = data[:at - 3] + struct.pack("<H", 1 + 8 * k) + b"\x02" + frame + data[at + ln:]
+        with pytest.raises(X.XfgStarkError) as e:
+            X.StarkProof.from_bytes(bad)
+        assert "OOD frame layout" in str(e.value), k
+        assert not X.XfgBurnMintVerifier().verify_with_public_inputs(bad, _statement(X, synthetic.REFERENCE_PACKAGE))
+    # an invalid field extension byte in the context
+    ext_at = 5 + struct.unpack_from("<H", data, 3)[0] + 1 + 8 + 3
+    for ext in (0, 4, 255):
+        bad = data[:ext_at] + bytes([ext]) + data[ext_at + 1:]
+        with pytest.raises(X.XfgStarkError) as e:
+            X.StarkProof.from_bytes(bad)
+        assert "invalid field extension" in str(e.value), ext
+
+
+def _set_elem(proof, at, value):
+    return proof[:at] + struct.pack("<Q", value) + proof[at + 8:]
+
+
+def test_noncanonical_elements_rejected(X):
+    """A value >= p in any element field of the proof is a deserialization error (winter-math
+    BaseElement::read_from), not arithmetic on a non-reduced operand (ADVICE r01)."""
+    P = 0xFFFFFFFF00000001
+    kws = synthetic.burn_inputs(5)
+    proof = _oracle_proof(kws, 256)
+    air = _statement(X, kws)
+    v = X.XfgBurnMintVerifier()
+    sec = _sections(proof)
+    # opened trace row, column 0 = burn amount (constant column, so its LDE value is small): v + p
+    at = sec["trace_rows"][0]
+    val = struct.unpack_from("<Q", proof, at)[0]
+    assert val == kws["burn_amount"] and val + P < 1 << 64
+    ok, err, _ = v.verify_with_details(_set_elem(proof, at, val + P), air)
+    assert not ok and err == 'ProofDeserializationError("invalid field element")', err
+    # the same value in the OOD frame: T_0(z) = burn for the constant column
+    at = sec["ood"][0]
+    assert struct.unpack_from("<Q", proof, at)[0] == kws["burn_amount"]
+    ok, err, _ = v.verify_with_details(_set_elem(proof, at, kws["burn_amount"] + P), air)
+    assert not ok and err == 'ProofDeserializationError("invalid field element")', err
+    # >= p (no canonical preimage needed) in each other element section
+    for name in ("constraint_rows", "hz", "fri_vals0", "remainder"):
+        at = sec[name][0]
+        bad = _set_elem(proof, at, 0xFFFFFFFFFFFFFFFF)
+        ok, err, _ = v.verify_with_details(bad, air)
+        assert not ok and err == 'ProofDeserializationError("invalid field element")', (name, err)
+        with pytest.raises(X.XfgStarkError):
+            X.StarkProof.from_bytes(bad)
+    # p itself is non-canonical too; p - 1 parses (and then fails a check, not the parser)
+    at = sec["remainder"][0]
+    ok, err, _ = v.verify_with_details(_set_elem(proof, at, P), air)
+    assert not ok and err.startswith("ProofDeserializationError"), err
+    ok, err, _ = v.verify_with_details(_set_elem(proof, at, P - 1), air)
+    assert not ok and err.startswith("FriVerificationFailed"), err
+
+
+def test_from_bytes_remainder_len_counts_elements(X):
+    for kw in (dict(), dict(field_extension=2)):
+        kws = synthetic.burn_inputs(9)
+        proof = _oracle_proof(kws, 256, **kw)
+        p = X.StarkProof.from_bytes(proof)
+        de = kw.get("field_extension", 1)
+        assert p.remainder_len == _sections(proof)["remainder"][1] // (8 * de)
+        # (31 + 1) coefficients at most: remainder degree bound of the reference options
+        assert p.remainder_len <= 32
 
 
 def test_verifier_accepts_golden_fixture(X):

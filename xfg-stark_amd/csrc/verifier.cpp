@@ -60,6 +60,15 @@ static bool read_span(Reader& r, int len_bytes, Span& s) {
     s.p = r.take(s.n);
     return !r.bad;
 }
+// every field element of a proof is canonical: winter-math 0.8 BaseElement::read_from rejects a
+// value >= p, so a non-canonical encoding fails deserialization here too (and the field code on
+// both the host and the GPU verifier may then assume canonical operands)
+static bool canonical_elems(const Span& s) {
+    if (s.n % 8) return false;
+    for (size_t i = 0; i < s.n / 8; i++)
+        if (s.elem(i) >= P) return false;
+    return true;
+}
 
 // returns "" on success, else the ProofDeserializationError text
 std::string parse_proof(const uint8_t* bytes, size_t len, ParsedProof& pf) {
@@ -80,6 +89,8 @@ std::string parse_proof(const uint8_t* bytes, size_t len, ParsedProof& pf) {
     if (r.bad) return "ProofDeserializationError(\"context: unexpected end of input\")";
     if (mlen != 8 || modulus != xfg::P) return "InconsistentBaseField";
     if (pf.logn < 3 || pf.logn > 32) return "ProofDeserializationError(\"context: invalid trace length\")";
+    // FieldExtension::{None, Quadratic, Cubic} = 1, 2, 3 (winter-air 0.8 ProofOptions::read_from)
+    if (pf.o.ext < 1 || pf.o.ext > 3) return "ProofDeserializationError(\"context: invalid field extension\")";
     pf.num_unique = r.u(1);
     const u64 clen = r.u(2);
     const uint8_t* c = r.take(clen);
@@ -96,21 +107,28 @@ std::string parse_proof(const uint8_t* bytes, size_t len, ParsedProof& pf) {
         return "ProofDeserializationError(\"constraint query paths\")";
     Span hz;
     if (!read_span(r, 2, pf.ood) || !read_span(r, 2, hz)) return "ProofDeserializationError(\"OOD frame\")";
-    const size_t esz = pf.o.ext == 2 ? 16 : 8;  // bytes per E element
-    if (pf.ood.n < 1 || pf.ood.p[0] != 2 || (pf.ood.n - 1) % (2 * esz) || hz.n != esz)
+    const size_t esz = 8 * (size_t)pf.o.ext;  // bytes per E element
+    // frame of two rows (current, next) of `width` E values each: exactly that many, so every
+    // reader of the frame (verifier, xfg_proof_parse) stays inside the proof bytes
+    if (pf.ood.n != 1 + 2 * pf.width * esz || pf.ood.p[0] != 2 || hz.n != esz)
         return "ProofDeserializationError(\"OOD frame layout\")";
     pf.ood.p += 1;
     pf.ood.n -= 1;
     pf.hz = hz;
+    if (!canonical_elems(pf.trace_rows) || !canonical_elems(pf.constraint_rows) || !canonical_elems(pf.ood) ||
+        !canonical_elems(pf.hz))
+        return "ProofDeserializationError(\"invalid field element\")";
     const u64 nl = r.u(1);
     pf.fri_vals.resize(nl);
     pf.fri_paths.resize(nl);
     for (u64 l = 0; l < nl; l++) {
         if (!read_span(r, 4, pf.fri_vals[l])) return "ProofDeserializationError(\"FRI layer values\")";
+        if (!canonical_elems(pf.fri_vals[l])) return "ProofDeserializationError(\"invalid field element\")";
         const u64 pl = r.u(4);
         if (r.bad || !read_paths(r, pl, pf.fri_paths[l])) return "ProofDeserializationError(\"FRI layer paths\")";
     }
     if (!read_span(r, 2, pf.fri_rem) || pf.fri_rem.n % esz) return "ProofDeserializationError(\"FRI remainder\")";
+    if (!canonical_elems(pf.fri_rem)) return "ProofDeserializationError(\"invalid field element\")";
     pf.partitions = r.u(1);
     pf.nonce = r.u(8);
     if (r.bad) return "ProofDeserializationError(\"unexpected end of input\")";
@@ -619,12 +637,14 @@ int xfg_proof_parse(const uint8_t* proof, size_t len, xfg_proof_info* info, char
     info->options.fri_remainder_max_degree = (uint32_t)pf.o.remdeg;
     info->num_unique_queries = (uint32_t)pf.num_unique;
     info->num_fri_layers = (uint32_t)pf.fri_vals.size();
-    info->remainder_len = (uint32_t)(pf.fri_rem.n / 8);
+    const size_t de = (size_t)pf.o.ext;  // coordinates per E element (parse_proof: 1..3)
+    info->remainder_len = (uint32_t)(pf.fri_rem.n / (8 * de));
     info->pow_nonce = pf.nonce;
     info->size = pf.size;
     for (size_t i = 0; i < 2 && i < pf.com.size(); i++) memcpy(i ? info->constraint_root : info->trace_root, pf.com[i].w, 32);
-    const int de = pf.o.ext == 2 ? 2 : 1;  // with an extension: first coordinates
-    for (int k = 0; k < 14; k++) info->ood_trace[k] = pf.ood.elem((size_t)k * de);
+    // with an extension: first coordinates; a frame narrower than 7 columns leaves the rest 0
+    const size_t frame = pf.ood.n / (8 * de);
+    for (size_t k = 0; k < 14 && k < frame; k++) info->ood_trace[k] = pf.ood.elem(k * de);
     info->ood_composition = pf.hz.elem(0);
     return XFG_OK;
 }

@@ -186,6 +186,11 @@ class StarkProof:
         return self._parse().num_fri_layers
 
     @property
+    def remainder_len(self):
+        """FRI remainder coefficients (E elements)"""
+        return self._parse().remainder_len
+
+    @property
     def pow_nonce(self):
         return self._parse().pow_nonce
 
