@@ -72,7 +72,7 @@ __device__ __forceinline__ u64 mul_pow2(u64 x) {
 }
 // exponent of two of w_{2^k} (Winterfell's roots: get_root_of_unity(k))
 __host__ __device__ constexpr int root_exp2(int k) {
-    return k == 1 ? 96 : k == 2 ? 48 : k == 3 ? 120 : k == 4 ? 156 : 0;
+    return k == 1 ? 96 : k == 2 ? 48 : k == 3 ? 120 : k == 4 ? 156 : k == 5 ? 78 : k == 6 ? 39 : 0;
 }
 __host__ __device__ constexpr int brev_c(int x, int bits) {
     int r = 0;
@@ -180,16 +180,17 @@ __device__ __forceinline__ u64 tw_get(const Tables& T, int k, u64 e, bool inv) {
 }
 
 // ---------------------------------------------------------------- one Stockham step
-// Radix 2^LOGR step of a size-2^LOGS DFT on 2^lognseq sequences. Group g of the step is
+// Radix 2^LOGR step of a size-2^LOGS DFT on 2^lognseq sequences, 2^LOGE elements per thread
+// (2^(LOGE - LOGR) groups). Group g of the step is
 // (seq, j); SEQ_FAST maps consecutive lanes to consecutive sequences, otherwise to consecutive j.
 // ld(seq, j, o) reads logical element i = j + o of a sequence (o = r * G, uniform across the
 // wave); st(seq, base, stride, v) receives the R
 // outputs of a group, which belong at logical positions base + r * stride.
 // IN_PLACE: every load of the step completes (barrier) before any store.
 // pf(q, seq, base, stride) runs before the group's loads (prefetch of what st will need).
-template <int LOGS, int LOGR, bool INV, bool SEQ_FAST, bool IN_PLACE, int NT, class LD, class ST, class PF>
+template <int LOGS, int LOGR, int LOGE, bool INV, bool SEQ_FAST, bool IN_PLACE, int NT, class LD, class ST, class PF>
 __device__ __forceinline__ void stockham(int lognseq, int Ns, const u64* ltw, LD ld, ST st, PF pf) {
-    constexpr int S = 1 << LOGS, R = 1 << LOGR, G = S / R, PER = 16 / R;
+    constexpr int S = 1 << LOGS, R = 1 << LOGR, G = S / R, PER = (1 << LOGE) / R;
     const int nseq = 1 << lognseq;
     const int groups = nseq * G;
     u64 v[PER][R];
@@ -223,38 +224,42 @@ __device__ __forceinline__ void stockham(int lognseq, int Ns, const u64* ltw, LD
     }
 }
 
-// steps of a size-2^LOGS DFT: the remainder radix first, then radix 16. (Remainder last would
-// save general twiddle multiplies -- radix 2 last multiplies 1/2 of the elements where radix 2
-// first makes the next radix-16 step multiply 15/16 -- but its narrow final step stores measured
-// 25 % slower at 2^20: 2.14 vs 1.72 ms per configs[4] trace LDE, same box.)
-template <int LOGS>
+// steps of a size-2^LOGS DFT with 2^LOGE elements per thread: the remainder radix first, then
+// radix 2^LOGE (16, or 32 where that saves a general-twiddle step: a size-1024 DFT is 32 x 32
+// -- one twiddle multiply per element -- instead of 4 x 16 x 16 -- two; the radix-32 butterfly
+// twiddles are still shifts, w_32 = 2^78). (Remainder last would save general twiddle multiplies
+// -- radix 2 last multiplies 1/2 of the elements where radix 2 first makes the next radix-16 step
+// multiply 15/16 -- but its narrow final step stores measured 25 % slower at 2^20: 2.14 vs
+// 1.72 ms per configs[4] trace LDE, same box.)
+template <int LOGS, int LOGE = 4>
 struct Plan {
-    static constexpr int REM = LOGS % 4;
-    static constexpr int NSTEP = LOGS / 4 + (REM ? 1 : 0);
-    static constexpr int FIRST_LOGR = REM ? REM : 4;
+    static constexpr int REM = LOGS % LOGE;
+    static constexpr int NSTEP = LOGS / LOGE + (REM ? 1 : 0);
+    static constexpr int FIRST_LOGR = REM ? REM : LOGE;
     // radix of the step that produces the final outputs
-    static constexpr int LAST_LOGR = NSTEP == 1 ? FIRST_LOGR : 4;
+    static constexpr int LAST_LOGR = NSTEP == 1 ? FIRST_LOGR : LOGE;
     static constexpr int LAST_R = 1 << LAST_LOGR;
 };
 
 // Whole DFT of every sequence: the first step loads with ldg (global), middle steps run in the
 // LDS tile, the last step stores with stg (global). A one-step DFT goes global -> global.
 // stg(q, seq, base, stride, v) stores group q's outputs; pf as in stockham, for the last step
-template <int LOGS, bool INV, bool FIRST_SEQ_FAST, int NT, class LDG, class STG, class PF>
+template <int LOGS, int LOGE, bool INV, bool FIRST_SEQ_FAST, int NT, class LDG, class STG, class PF>
 __device__ __forceinline__ void pass_dft(u64* tile, int lognseq, const u64* ltw, LDG ldg, STG stg, PF pf) {
-    using PL = Plan<LOGS>;
-    constexpr int PITCH = row_pitch(1 << LOGS);
+    using PL = Plan<LOGS, LOGE>;
+    constexpr int PITCH = row_pitch(1 << LOGS), E = 1 << LOGE;
     auto nopf = [](int, int, int, int) {};
     if constexpr (PL::NSTEP == 1) {
-        stockham<LOGS, PL::FIRST_LOGR, INV, FIRST_SEQ_FAST, false, NT>(lognseq, 1, ltw, ldg, stg, pf);
+        stockham<LOGS, PL::FIRST_LOGR, LOGE, INV, FIRST_SEQ_FAST, false, NT>(lognseq, 1, ltw, ldg, stg, pf);
     } else {
-        stockham<LOGS, PL::FIRST_LOGR, INV, FIRST_SEQ_FAST, false, NT>(
+        stockham<LOGS, PL::FIRST_LOGR, LOGE, INV, FIRST_SEQ_FAST, false, NT>(
             lognseq, 1, ltw, ldg, [&](int, int seq, int base, int stride, u64* v) {
                 u64* row = tile + seq * PITCH;
 #pragma unroll
                 for (int r = 0; r < (1 << PL::FIRST_LOGR); r++) {
-                    // radix-16 first step: base = 16 j, stride 1 -> the 16 outputs are contiguous
-                    if constexpr (PL::FIRST_LOGR == 4) row[phys(base) + r] = v[r];
+                    // full-radix first step: base = R j, stride 1 -> the R outputs are contiguous
+                    // (a multiple of 16 elements: the pad words fall at fixed offsets)
+                    if constexpr (PL::FIRST_LOGR >= 4) row[phys(base) + r + (r >> 4)] = v[r];
                     else row[phys(base + r * stride)] = v[r];
                 }
             },
@@ -263,18 +268,18 @@ __device__ __forceinline__ void pass_dft(u64* tile, int lognseq, const u64* ltw,
         int Ns = 1 << PL::FIRST_LOGR;
 #pragma unroll
         for (int st = 1; st < PL::NSTEP - 1; st++) {
-            stockham<LOGS, 4, INV, true, true, NT>(
+            stockham<LOGS, LOGE, LOGE, INV, true, true, NT>(
                 lognseq, Ns, ltw, [&](int seq, int j, int o) { return tile[seq * PITCH + phys2(j, o)]; },
                 [&](int, int seq, int base, int stride, u64* v) {
                     u64* row = tile + seq * PITCH;
 #pragma unroll
-                    for (int r = 0; r < 16; r++) row[phys2(base, r * stride)] = v[r];
+                    for (int r = 0; r < E; r++) row[phys2(base, r * stride)] = v[r];
                 },
                 nopf);
             __syncthreads();
-            Ns <<= 4;
+            Ns <<= LOGE;
         }
-        stockham<LOGS, PL::LAST_LOGR, INV, true, false, NT>(
+        stockham<LOGS, PL::LAST_LOGR, LOGE, INV, true, false, NT>(
             lognseq, Ns, ltw, [&](int seq, int j, int o) { return tile[seq * PITCH + phys2(j, o)]; }, stg, pf);
         __syncthreads();
     }
@@ -316,13 +321,14 @@ __device__ __forceinline__ void xcd_block(bool on, int& bx, int& by) {
 // forward, coset t: x[j1] = c[C j1 + j2] * 7^(C j1) w_(beta R)^(t j1)
 //   y[t][k1][j2] = X[k1] * 7^j2 * w_N^(j2 (t + beta k1))
 // inverse: y[k1][j2] = X[k1] * w_n^-(j2 k1)
-// LOGT = log2 threads: 8 (4096-element tiles, several blocks per CU) or 10 (16384-element tiles
-// in up to 155 KiB of LDS, one block per CU: 16 columns per tile even at R = 1024)
-template <int LOGR, bool INV, int LOGT>
-__global__ __launch_bounds__(1 << LOGT, 1 << (10 - LOGT)) void ntt_pass_a(NttArgs a) {
-    constexpr int R = 1 << LOGR, PITCH = row_pitch(R), RR = Plan<LOGR>::LAST_R, NT = 1 << LOGT;
+// LOGT = log2 threads, LOGE = log2 elements per thread: 2^(LOGT + LOGE)-element tiles, e.g.
+// 256 x 16 (several blocks per CU), 1024 x 16 or 512 x 32 (16384 elements in up to 155 KiB of
+// LDS, one block per CU: 16 columns per tile even at R = 1024)
+template <int LOGR, bool INV, int LOGT, int LOGE>
+__global__ __launch_bounds__(1 << LOGT, (1 << (10 - LOGT)) >> (LOGE - 4)) void ntt_pass_a(NttArgs a) {
+    constexpr int R = 1 << LOGR, PITCH = row_pitch(R), RR = Plan<LOGR, LOGE>::LAST_R, NT = 1 << LOGT;
     extern __shared__ u64 lds[];
-    const int logTC = (a.logC < LOGT + 4 - LOGR) ? a.logC : LOGT + 4 - LOGR;
+    const int logTC = (a.logC < LOGT + LOGE - LOGR) ? a.logC : LOGT + LOGE - LOGR;
     const int TC = 1 << logTC;
     u64* tile = lds;
     u64* ltw = lds + TC * PITCH;
@@ -351,7 +357,7 @@ __global__ __launch_bounds__(1 << LOGT, 1 << (10 - LOGT)) void ntt_pass_a(NttArg
     };
     // four-step twiddles from the table: loaded by pf before the last step's loads and butterflies,
     // so the table latency hides behind them; one multiply per element instead of two
-    constexpr int PERL = 16 / RR;
+    constexpr int PERL = (1 << LOGE) / RR;
     u64 tq[PERL][RR];
     const u64* tab = a.t4 ? a.t4 + (INV ? 0 : ((u64)t << a.logn)) + col0 : nullptr;
     const auto rtab = buf_rsrc(tab ? tab : y);
@@ -384,15 +390,15 @@ __global__ __launch_bounds__(1 << LOGT, 1 << (10 - LOGT)) void ntt_pass_a(NttArg
             if (r + 1 < RR) w = gl_mul(w, step);
         }
     };
-    pass_dft<LOGR, INV, true, NT>(tile, logTC, ltw, ldg, stg, pf);
+    pass_dft<LOGR, LOGE, INV, true, NT>(tile, logTC, ltw, ldg, stg, pf);
 }
 
 // ---------------------------------------------------------------- pass B: row DFTs (size C)
-template <int LOGC, bool INV, int LOGT>
+template <int LOGC, bool INV, int LOGT, int LOGE>
 __global__ __launch_bounds__(1 << LOGT) void ntt_pass_b(NttArgs a) {
-    constexpr int C = 1 << LOGC, RR = Plan<LOGC>::LAST_R, NT = 1 << LOGT;
+    constexpr int C = 1 << LOGC, RR = Plan<LOGC, LOGE>::LAST_R, NT = 1 << LOGT;
     extern __shared__ u64 lds[];
-    const int logTR = (a.logR < LOGT + 4 - LOGC) ? a.logR : LOGT + 4 - LOGC;
+    const int logTR = (a.logR < LOGT + LOGE - LOGC) ? a.logR : LOGT + LOGE - LOGC;
     const int TR = 1 << logTR;
     u64* tile = lds;
     u64* ltw = lds + TR * row_pitch(C);
@@ -423,7 +429,8 @@ __global__ __launch_bounds__(1 << LOGT) void ntt_pass_b(NttArgs a) {
     };
     // multi-step rows: first step along the row (coalesced loads); one-step rows: lanes along
     // sequences so the (final) global store is coalesced
-    pass_dft<LOGC, INV, (Plan<LOGC>::NSTEP == 1), NT>(tile, logTR, ltw, ldg, stg, [](int, int, int, int) {});
+    pass_dft<LOGC, LOGE, INV, (Plan<LOGC, LOGE>::NSTEP == 1), NT>(tile, logTR, ltw, ldg, stg,
+                                                                   [](int, int, int, int) {});
 }
 
 // ---------------------------------------------------------------- dispatch
@@ -439,13 +446,29 @@ __global__ __launch_bounds__(1 << LOGT) void ntt_pass_b(NttArgs a) {
         hipLaunchKernelGGL(KERNEL, g, dim3(NT), lds, s, a);                                                 \
     } while (0)
 template <bool INV>
-static void run_pass_a(int logR, int logT, dim3 g, size_t lds, hipStream_t s, const NttArgs& a) {
+static void run_pass_a(int logR, int logT, int logE, dim3 g, size_t lds, hipStream_t s, const NttArgs& a) {
 #define XFG_CASE_A(L) \
-    case L: XFG_NTT_LAUNCH((ntt_pass_a<L, INV, 8>), 256); break;
+    case L: XFG_NTT_LAUNCH((ntt_pass_a<L, INV, 8, 4>), 256); break;
 #define XFG_CASE_A10(L) \
-    case L: XFG_NTT_LAUNCH((ntt_pass_a<L, INV, 10>), 1024); break;
+    case L: XFG_NTT_LAUNCH((ntt_pass_a<L, INV, 10, 4>), 1024); break;
 #define XFG_CASE_A9(L) \
-    case L: XFG_NTT_LAUNCH((ntt_pass_a<L, INV, 9>), 512); break;
+    case L: XFG_NTT_LAUNCH((ntt_pass_a<L, INV, 9, 4>), 512); break;
+#define XFG_CASE_A5(L, T) \
+    case L: XFG_NTT_LAUNCH((ntt_pass_a<L, INV, T, 5>), (1 << T)); break;
+    if (logE == 5) {
+        if (logT == 9) {
+            switch (logR) {
+                XFG_CASE_A5(9, 9) XFG_CASE_A5(10, 9)
+                default: break;
+            }
+        } else {
+            switch (logR) {
+                XFG_CASE_A5(9, 8) XFG_CASE_A5(10, 8)
+                default: break;
+            }
+        }
+        return;
+    }
     if (logT == 10) {
         switch (logR) {
             XFG_CASE_A10(9) XFG_CASE_A10(10)
@@ -468,15 +491,32 @@ static void run_pass_a(int logR, int logT, dim3 g, size_t lds, hipStream_t s, co
 #undef XFG_CASE_A
 #undef XFG_CASE_A10
 #undef XFG_CASE_A9
+#undef XFG_CASE_A5
 }
 template <bool INV>
-static void run_pass_b(int logC, int logT, dim3 g, size_t lds, hipStream_t s, const NttArgs& a) {
+static void run_pass_b(int logC, int logT, int logE, dim3 g, size_t lds, hipStream_t s, const NttArgs& a) {
 #define XFG_CASE_B(L) \
-    case L: XFG_NTT_LAUNCH((ntt_pass_b<L, INV, 8>), 256); break;
+    case L: XFG_NTT_LAUNCH((ntt_pass_b<L, INV, 8, 4>), 256); break;
 #define XFG_CASE_B10(L) \
-    case L: XFG_NTT_LAUNCH((ntt_pass_b<L, INV, 10>), 1024); break;
+    case L: XFG_NTT_LAUNCH((ntt_pass_b<L, INV, 10, 4>), 1024); break;
 #define XFG_CASE_B9(L) \
-    case L: XFG_NTT_LAUNCH((ntt_pass_b<L, INV, 9>), 512); break;
+    case L: XFG_NTT_LAUNCH((ntt_pass_b<L, INV, 9, 4>), 512); break;
+#define XFG_CASE_B5(L, T) \
+    case L: XFG_NTT_LAUNCH((ntt_pass_b<L, INV, T, 5>), (1 << T)); break;
+    if (logE == 5) {
+        if (logT == 9) {
+            switch (logC) {
+                XFG_CASE_B5(9, 9) XFG_CASE_B5(10, 9)
+                default: break;
+            }
+        } else {
+            switch (logC) {
+                XFG_CASE_B5(9, 8) XFG_CASE_B5(10, 8)
+                default: break;
+            }
+        }
+        return;
+    }
     if (logT == 10) {
         switch (logC) {
             XFG_CASE_B10(9) XFG_CASE_B10(10) XFG_CASE_B10(11)
@@ -499,6 +539,7 @@ static void run_pass_b(int logC, int logT, dim3 g, size_t lds, hipStream_t s, co
 #undef XFG_CASE_B
 #undef XFG_CASE_B10
 #undef XFG_CASE_B9
+#undef XFG_CASE_B5
 }
 #undef XFG_NTT_LAUNCH
 
@@ -561,13 +602,25 @@ static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
         const char* v = getenv("XFG_NTT_LTB");
         return v && *v ? atoi(v) : 0;
     }();
+    // radix-32 steps (32 elements per thread) for pass sizes 2^9 and 2^10: 16 x 32 and 32 x 32
+    // instead of 2 x 16 x 16 and 4 x 16 x 16, one general-twiddle step fewer (XFG_NTT_E=4 disables)
+    static const bool e5_on = [] {
+        const char* v = getenv("XFG_NTT_E");
+        return !(v && *v == '4');
+    }();
+    const int eA = (e5_on && wide_on && a.logR >= 9 && a.logR <= 10 && a.logC >= 4) ? 5 : 4;
+    const int eB = (e5_on && wide_on && a.logC >= 9 && a.logC <= 10 && a.logR >= 3) ? 5 : 4;
     const bool capA = a.logR >= 9 && a.logR <= 10 && a.logC >= 4, capB = a.logC >= 9 && a.logC <= 11 && a.logR >= 4;
-    const int ltA = capA ? (force_lta >= 8 && force_lta <= 10 ? force_lta : (wide_on ? 10 : 8)) : 8;
+    int ltA = capA ? (force_lta >= 8 && force_lta <= 10 ? force_lta : (wide_on ? 10 : 8)) : 8;
     // pass B: 512 threads (8192 elements, <= 78 KiB, two blocks per CU) up to C = 1024 -- the second
     // block hides the first one's barriers and load latency; 1024 threads at C = 2048
-    const int ltB = capB ? (force_ltb >= 8 && force_ltb <= 10 ? force_ltb : (wide_on ? (a.logC <= 10 ? 9 : 10) : 8)) : 8;
-    const int logTC = a.logC < ltA + 4 - a.logR ? a.logC : ltA + 4 - a.logR;
-    const int logTR = a.logR < ltB + 4 - a.logC ? a.logR : ltB + 4 - a.logC;
+    int ltB = capB ? (force_ltb >= 8 && force_ltb <= 10 ? force_ltb : (wide_on ? (a.logC <= 10 ? 9 : 10) : 8)) : 8;
+    // radix-32 tiles: pass A 16 columns (512 threads at R = 1024, 256 at R = 512), pass B 8192
+    // elements (256 threads, two blocks per CU); forced thread counts limited to 256 / 512
+    if (eA == 5) ltA = (force_lta == 8 || force_lta == 9) ? force_lta : a.logR - 1;
+    if (eB == 5) ltB = (force_ltb == 8 || force_ltb == 9) ? force_ltb : 8;
+    const int logTC = a.logC < ltA + eA - a.logR ? a.logC : ltA + eA - a.logR;
+    const int logTR = a.logR < ltB + eB - a.logC ? a.logR : ltB + eB - a.logC;
     const int ncos = inv ? 1 : (1 << a.logbeta);
     size_t lds_a = ((size_t)(1 << logTC) * row_pitch(R) + 2 * R) * sizeof(u64);
     size_t lds_b = ((size_t)(1 << logTR) * row_pitch(C) + C) * sizeof(u64);
@@ -580,11 +633,11 @@ static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
     }();
     a.xcd = xcd_on ? ((logTC < 4 ? 1 : 0) | (logTR < 4 ? 2 : 0)) : 0;
     if (inv) {
-        run_pass_a<true>(a.logR, ltA, ga, lds_a, s, a);
-        run_pass_b<true>(a.logC, ltB, gb, lds_b, s, a);
+        run_pass_a<true>(a.logR, ltA, eA, ga, lds_a, s, a);
+        run_pass_b<true>(a.logC, ltB, eB, gb, lds_b, s, a);
     } else {
-        run_pass_a<false>(a.logR, ltA, ga, lds_a, s, a);
-        run_pass_b<false>(a.logC, ltB, gb, lds_b, s, a);
+        run_pass_a<false>(a.logR, ltA, eA, ga, lds_a, s, a);
+        run_pass_b<false>(a.logC, ltB, eB, gb, lds_b, s, a);
     }
 }
 
