@@ -285,6 +285,7 @@ __device__ __forceinline__ void pass_dft(u64* tile, int lognseq, const u64* ltw,
     }
 }
 
+__host__ __device__ u64 fourstep_main(int logn, int logbeta);
 struct NttArgs {
     const u64* in;
     u64* y;
@@ -341,11 +342,20 @@ __global__ __launch_bounds__(1 << LOGT, (1 << (10 - LOGT)) >> (LOGE - 4)) void n
     const u64 n = 1ULL << a.logn;
     const int logN = a.logn + a.logbeta;
     const u64 maskN = (1ULL << logN) - 1;
-    for (int i = threadIdx.x; i < R; i += NT) {
-        ltw[i] = tw_get(a.T, LOGR, i, INV);
-        if (!INV)
-            pre[i] = gl_mul(a.T.pow7[(u64)i << a.logC],
-                            tw_get(a.T, LOGR + a.logbeta, ((u64)t * i) & ((1ULL << (LOGR + a.logbeta)) - 1), false));
+    if (a.t4) {
+        // contiguous per-size tables behind the four-step table (build_fourstep): coalesced loads
+        const u64* pt4 = a.t4 + fourstep_main(a.logn, INV ? -1 : a.logbeta);
+        for (int i = threadIdx.x; i < R; i += NT) {
+            ltw[i] = pt4[i];
+            if (!INV) pre[i] = pt4[R + (1 << a.logC) + t * R + i];
+        }
+    } else {
+        for (int i = threadIdx.x; i < R; i += NT) {
+            ltw[i] = tw_get(a.T, LOGR, i, INV);
+            if (!INV)
+                pre[i] = gl_mul(a.T.pow7[(u64)i << a.logC],
+                                tw_get(a.T, LOGR + a.logbeta, ((u64)t * i) & ((1ULL << (LOGR + a.logbeta)) - 1), false));
+        }
     }
     __syncthreads();
     const u64* in = a.in + (u64)poly * a.in_stride;
@@ -406,7 +416,12 @@ __global__ __launch_bounds__(1 << LOGT) void ntt_pass_b(NttArgs a) {
     xcd_block(a.xcd & 2, bx, by);
     const int pt = by, k10 = bx * TR;
     const u64 n = 1ULL << a.logn;
-    for (int i = threadIdx.x; i < C; i += NT) ltw[i] = tw_get(a.T, LOGC, i, INV);
+    if (a.t4) {
+        const u64* pt4 = a.t4 + fourstep_main(a.logn, INV ? -1 : a.logbeta) + (1 << a.logR);
+        for (int i = threadIdx.x; i < C; i += NT) ltw[i] = pt4[i];
+    } else {
+        for (int i = threadIdx.x; i < C; i += NT) ltw[i] = tw_get(a.T, LOGC, i, INV);
+    }
     __syncthreads();
     const u64* y = a.y + (u64)pt * n;
     auto ldg = [&](int seq, int j, int o) -> u64 { return y[((u64)(k10 + seq) << LOGC) + j + o]; };
@@ -574,13 +589,36 @@ __global__ void fourstep_kernel(u64* out, int logn, int logbeta, int logC, u64 s
         out[i] = gl_mul(T.pow7[j2], tw_get(T, logN, (j2 * (t + (k1 << logbeta))) & ((1ULL << logN) - 1), false));
     }
 }
-u64 fourstep_size(int logn, int logbeta) { return 1ULL << (logn + (logbeta > 0 ? logbeta : 0)); }
+// pass tables appended to a four-step table: w_R^(+-i) (i < R), w_C^(+-i) (i < C), and for the
+// forward LDE the coset pre-factors 7^(C i) w_(beta R)^(t i) at [t][i] -- what every pass block
+// would otherwise gather from the master tables at its start
+__global__ void pass_tables_kernel(u64* out, int logn, int logbeta, int logR, int logC, Tables T) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    const u64 R = 1ULL << logR, C = 1ULL << logC;
+    const bool inv = logbeta < 0;
+    if (i < R) {
+        out[i] = tw_get(T, logR, i, inv);
+    } else if (i < R + C) {
+        out[i] = tw_get(T, logC, i - R, inv);
+    } else if (!inv && i < R + C + (R << logbeta)) {
+        const u64 t = (i - R - C) >> logR, j = (i - R - C) & (R - 1);
+        out[i] = gl_mul(T.pow7[j << logC], tw_get(T, logR + logbeta, (t * j) & ((1ULL << (logR + logbeta)) - 1), false));
+    }
+}
+__host__ __device__ u64 fourstep_main(int logn, int logbeta) { return 1ULL << (logn + (logbeta > 0 ? logbeta : 0)); }
+u64 fourstep_size(int logn, int logbeta) {
+    int logR, logC;
+    ntt_split(logn, logR, logC);
+    return fourstep_main(logn, logbeta) + (1ULL << logR) + (1ULL << logC) + (logbeta >= 0 ? (1ULL << (logR + logbeta)) : 0);
+}
 void build_fourstep(u64* out, int logn, int logbeta, const Tables& T, hipStream_t s) {
     int logR, logC;
     ntt_split(logn, logR, logC);
-    const u64 cnt = fourstep_size(logn, logbeta);
+    const u64 cnt = fourstep_main(logn, logbeta), extra = fourstep_size(logn, logbeta) - cnt;
     hipLaunchKernelGGL(fourstep_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, out, logn, logbeta, logC,
                        gl_inv(1ULL << logn), T);
+    hipLaunchKernelGGL(pass_tables_kernel, dim3((unsigned)((extra + 255) / 256)), dim3(256), 0, s, out + cnt, logn,
+                       logbeta, logR, logC, T);
 }
 
 static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
