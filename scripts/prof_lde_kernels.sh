@@ -8,7 +8,7 @@ rm -rf $OUT && mkdir -p $OUT
 i=0
 for kv in $AB; do
   i=$((i+1))
-  (cd /tmp && env $kv timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/k$i -o k -- python3 $OLDPWD/scripts/lde_only.py 64) > $OUT/k$i.log 2>&1 || { echo "prof $kv failed"; tail -5 $OUT/k$i.log; exit 1; }
+  (cd /tmp && env ${kv//,/ } timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/k$i -o k -- python3 $OLDPWD/scripts/lde_only.py 64) > $OUT/k$i.log 2>&1 || { echo "prof $kv failed"; tail -5 $OUT/k$i.log; exit 1; }
   echo "== $kv"
   python3 - $OUT/k$i <<'PY'
 import csv, glob, sys
