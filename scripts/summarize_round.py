@@ -6,7 +6,7 @@ import csv, glob, json, os, sys
 from collections import defaultdict
 
 out = sys.argv[1]
-PA, PB = "void xfg::ntt_pass_a<8, false, 8>(xfg::NttArgs)", "void xfg::ntt_pass_b<8, false, 8>(xfg::NttArgs)"
+PA, PB = "void xfg::ntt_pass_a<8, false, 8, 4>(xfg::NttArgs)", "void xfg::ntt_pass_b<8, false, 8, 4>(xfg::NttArgs)"
 LDE_GRID_A = 14680064  # grid of pass A for 7 columns x 64 proofs x 8 cosets (n = 2^16)
 
 def rows(pattern):
