@@ -403,6 +403,66 @@ __global__ __launch_bounds__(1 << LOGT, (1 << (10 - LOGT)) >> (LOGE - 4)) void n
     pass_dft<LOGR, LOGE, INV, true, NT>(tile, logTC, ltw, ldg, stg, pf);
 }
 
+// ---------------------------------------------------------------- pass A, all cosets per block
+// The beta cosets of one column tile read the same coefficients: one block loads the tile once
+// (16 values per thread, kept in registers) and runs the column DFTs of every coset from them,
+// refilling only the coset pre-factors between cosets. Coefficient loads drop beta-fold and their
+// latency is paid once per tile instead of once per coset. Forward LDE with the four-step table,
+// one first-step group per thread (256 x 16 tiles of R = 256: 16 columns).
+template <int LOGR>
+__global__ __launch_bounds__(256, 3) void ntt_pass_a_cos(NttArgs a) {
+    constexpr int LOGT = 8, LOGE = 4, NT = 1 << LOGT, R = 1 << LOGR, PITCH = row_pitch(R);
+    using PL = Plan<LOGR, LOGE>;
+    constexpr int R1 = 1 << PL::FIRST_LOGR, G1 = R / R1, RR = PL::LAST_R;
+    static_assert((1 << LOGE) / R1 == 1, "one first-step group per thread");
+    extern __shared__ u64 lds[];
+    const int logTC = (a.logC < LOGT + LOGE - LOGR) ? a.logC : LOGT + LOGE - LOGR;
+    const int TC = 1 << logTC;
+    u64* tile = lds;
+    u64* ltw = lds + TC * PITCH;
+    u64* pre = ltw + R;
+    const int poly = blockIdx.y, col0 = blockIdx.x * TC;
+    const u64 n = 1ULL << a.logn;
+    const int beta = 1 << a.logbeta;
+    const u64* pt4 = a.t4 + fourstep_main(a.logn, a.logbeta);
+    const u64* pre_all = pt4 + R + (1 << a.logC);  // [t][R]
+    for (int i = threadIdx.x; i < R; i += NT) {
+        ltw[i] = pt4[i];
+        pre[i] = pre_all[i];
+    }
+    // this thread's first-step group (stockham, SEQ_FAST, q = 0): its R1 coefficients, loaded once
+    const int g = threadIdx.x, seq0 = g & (TC - 1), j0 = g >> logTC;
+    const auto rin = buf_rsrc(a.in + (u64)poly * a.in_stride + col0);
+    u64 raw[R1];
+#pragma unroll
+    for (int r = 0; r < R1; r++) raw[r] = buf_ld(rin, (((u32)j0 << a.logC) + seq0) * 8, ((u32)(r * G1) << a.logC) * 8);
+    __syncthreads();
+    for (int t = 0; t < beta; t++) {
+        const int pt = poly * beta + t;
+        // next coset's pre-factor, loaded now, stored after this coset's last barrier
+        const u64 pre_next = (t + 1 < beta && threadIdx.x < R) ? pre_all[(t + 1) * R + threadIdx.x] : 0;
+        const auto ry = buf_rsrc(a.y + (u64)pt * n + col0);
+        const auto rtab = buf_rsrc(a.t4 + ((u64)t << a.logn) + col0);
+        auto ldg = [&](int, int j, int o) -> u64 { return gl_mul(raw[o / G1], pre[j + o]); };
+        u64 tq[RR];
+        auto pf = [&](int, int seq, int base, int stride) {
+            const u32 vo = (((u32)base << a.logC) + seq) * 8;
+#pragma unroll
+            for (int r = 0; r < RR; r++) tq[r] = buf_ld(rtab, vo, ((u32)(r * stride) << a.logC) * 8);
+        };
+        auto stg = [&](int, int seq, int base, int stride, u64* v) {
+            const u32 vo = (((u32)base << a.logC) + seq) * 8;
+#pragma unroll
+            for (int r = 0; r < RR; r++) buf_st(ry, vo, ((u32)(r * stride) << a.logC) * 8, gl_mul(v[r], tq[r]));
+        };
+        pass_dft<LOGR, LOGE, false, true, NT>(tile, logTC, ltw, ldg, stg, pf);  // ends with a barrier
+        if (t + 1 < beta) {
+            if (threadIdx.x < R) pre[threadIdx.x] = pre_next;
+            __syncthreads();
+        }
+    }
+}
+
 // ---------------------------------------------------------------- pass B: row DFTs (size C)
 template <int LOGC, bool INV, int LOGT, int LOGE>
 __global__ __launch_bounds__(1 << LOGT) void ntt_pass_b(NttArgs a) {
@@ -674,7 +734,15 @@ static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
         run_pass_a<true>(a.logR, ltA, eA, ga, lds_a, s, a);
         run_pass_b<true>(a.logC, ltB, eB, gb, lds_b, s, a);
     } else {
-        run_pass_a<false>(a.logR, ltA, eA, ga, lds_a, s, a);
+        // all cosets of a column tile in one block (ntt_pass_a_cos); XFG_NTT_COS=0 disables
+        static const bool cos_on = [] {
+            const char* v = getenv("XFG_NTT_COS");
+            return !(v && *v == '0');
+        }();
+        if (cos_on && a.t4 && a.logR == 8 && ltA == 8 && eA == 4 && !(a.xcd & 1))
+            hipLaunchKernelGGL(ntt_pass_a_cos<8>, dim3(C >> logTC, npoly), dim3(256), lds_a, s, a);
+        else
+            run_pass_a<false>(a.logR, ltA, eA, ga, lds_a, s, a);
         run_pass_b<false>(a.logC, ltB, eB, gb, lds_b, s, a);
     }
 }
