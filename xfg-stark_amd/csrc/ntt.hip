@@ -298,6 +298,7 @@ struct NttArgs {
     u64 keep;     // inverse: coefficients written
     const u64* t4;  // four-step twiddle table (FourStep) or nullptr
     int xcd;        // 1: XCD-contiguous block order (see xcd_block)
+    int tq_b;       // forward: pass B applies the four-step twiddles as it loads (ntt_pass_a_cos)
     Tables T;
 };
 
@@ -442,20 +443,15 @@ __global__ __launch_bounds__(256, 3) void ntt_pass_a_cos(NttArgs a) {
         // next coset's pre-factor, loaded now, stored after this coset's last barrier
         const u64 pre_next = (t + 1 < beta && threadIdx.x < R) ? pre_all[(t + 1) * R + threadIdx.x] : 0;
         const auto ry = buf_rsrc(a.y + (u64)pt * n + col0);
-        const auto rtab = buf_rsrc(a.t4 + ((u64)t << a.logn) + col0);
         auto ldg = [&](int, int j, int o) -> u64 { return gl_mul(raw[o / G1], pre[j + o]); };
-        u64 tq[RR];
-        auto pf = [&](int, int seq, int base, int stride) {
-            const u32 vo = (((u32)base << a.logC) + seq) * 8;
-#pragma unroll
-            for (int r = 0; r < RR; r++) tq[r] = buf_ld(rtab, vo, ((u32)(r * stride) << a.logC) * 8);
-        };
+        // the four-step twiddles are applied by pass B as it loads (a.tq_b): the intermediate is
+        // stored weakly reduced, pass B's multiply canonicalises it
         auto stg = [&](int, int seq, int base, int stride, u64* v) {
             const u32 vo = (((u32)base << a.logC) + seq) * 8;
 #pragma unroll
-            for (int r = 0; r < RR; r++) buf_st(ry, vo, ((u32)(r * stride) << a.logC) * 8, gl_mul(v[r], tq[r]));
+            for (int r = 0; r < RR; r++) buf_st(ry, vo, ((u32)(r * stride) << a.logC) * 8, v[r]);
         };
-        pass_dft<LOGR, LOGE, false, true, NT>(tile, logTC, ltw, ldg, stg, pf);  // ends with a barrier
+        pass_dft<LOGR, LOGE, false, true, NT>(tile, logTC, ltw, ldg, stg, [](int, int, int, int) {});  // ends with a barrier
         if (t + 1 < beta) {
             if (threadIdx.x < R) pre[threadIdx.x] = pre_next;
             __syncthreads();
@@ -484,7 +480,35 @@ __global__ __launch_bounds__(1 << LOGT) void ntt_pass_b(NttArgs a) {
     }
     __syncthreads();
     const u64* y = a.y + (u64)pt * n;
-    auto ldg = [&](int seq, int j, int o) -> u64 { return y[((u64)(k10 + seq) << LOGC) + j + o]; };
+    // four-step twiddles at the load when pass A left them out (a.tq_b): the table has the
+    // intermediate's [k1][j2] layout, so its loads are as coalesced as the data's
+    const u64* tqb = (!INV && a.tq_b) ? a.t4 + ((u64)(pt & ((1 << a.logbeta) - 1)) << a.logn) : nullptr;
+    // with the twiddles, all of a thread's first-step loads (data and table) are issued before the
+    // first multiply (a load next to its multiply would be waited for one at a time: the field
+    // primitives are asm statements the scheduler does not move loads across). One first-step group
+    // per thread, lanes along the row (multi-step rows of 16-element threads).
+    using PLB = Plan<LOGC, LOGE>;
+    constexpr int R1 = 1 << PLB::FIRST_LOGR, G1 = C / R1;
+    constexpr bool PRE = !INV && PLB::NSTEP > 1 && (1 << LOGE) == R1;
+    u64 yv[PRE ? R1 : 1], tv[PRE ? R1 : 1];
+    if constexpr (PRE) {
+        if (tqb) {
+            const int seq0 = threadIdx.x / G1, j0 = threadIdx.x % G1;
+            const u64 i0 = ((u64)(k10 + seq0) << LOGC) + j0;
+#pragma unroll
+            for (int r = 0; r < R1; r++) {
+                yv[r] = y[i0 + r * G1];
+                tv[r] = tqb[i0 + r * G1];
+            }
+        }
+    }
+    auto ldg = [&](int seq, int j, int o) -> u64 {
+        if constexpr (PRE) {
+            if (tqb) return gl_mul(yv[o / G1], tv[o / G1]);
+        }
+        const u64 i = ((u64)(k10 + seq) << LOGC) + j + o;
+        return tqb ? gl_mul(y[i], tqb[i]) : y[i];
+    };
     const auto rout = buf_rsrc(a.out + (u64)pt * n + k10);
     auto stg = [&](int, int seq, int base, int stride, u64* v) {
 #pragma unroll
@@ -739,9 +763,10 @@ static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
             const char* v = getenv("XFG_NTT_COS");
             return !(v && *v == '0');
         }();
-        if (cos_on && a.t4 && a.logR == 8 && ltA == 8 && eA == 4 && !(a.xcd & 1))
+        if (cos_on && a.t4 && a.logR == 8 && ltA == 8 && eA == 4 && !(a.xcd & 1)) {
+            a.tq_b = 1;
             hipLaunchKernelGGL(ntt_pass_a_cos<8>, dim3(C >> logTC, npoly), dim3(256), lds_a, s, a);
-        else
+        } else
             run_pass_a<false>(a.logR, ltA, eA, ga, lds_a, s, a);
         run_pass_b<false>(a.logC, ltB, eB, gb, lds_b, s, a);
     }
