@@ -312,6 +312,9 @@ __global__ __launch_bounds__(256) void constraint_eval_kernel(CeArgs a) {
 #pragma unroll
     for (int c = 0; c < 7; c++) cur[c] = lde[(((u64)c << a.logbeta) + t) * n + m];
     const u64 nxt4 = lde[((4ULL << a.logbeta) + t) * n + mn];
+    // divisor inverses loaded with the frame (not next to the multiplies that use them)
+    const u64 di = par * n + m;
+    const u64 dv0 = a.div[di], dv1 = a.div[nce + di], dv2 = a.div[2 * nce + di];
     // XfgBurnMintAir::evaluate_transition (reference src/burn_mint_air.rs:335-378)
     const u64 std_burn = 8000000ULL, large_burn = 8000000000ULL;
     u64 r[7];
@@ -332,10 +335,9 @@ __global__ __launch_bounds__(256) void constraint_eval_kernel(CeArgs a) {
 #pragma unroll
     for (int c = 0; c < 7; c++) b0 = fe_add(b0, fe_mulb(F::load(co + (7 + c) * D), gl_sub(cur[c], v0[c])));
     const F b1 = fe_mulb(F::load(co + 14 * D), gl_sub(cur[4], 3));
-    const u64 di = par * n + m;
-    F val = fe_mulb(tr, a.div[di]);
-    val = fe_add(val, fe_mulb(b0, a.div[nce + di]));
-    val = fe_add(val, fe_mulb(b1, a.div[2 * nce + di]));
+    F val = fe_mulb(tr, dv0);
+    val = fe_add(val, fe_mulb(b0, dv1));
+    val = fe_add(val, fe_mulb(b1, dv2));
 #pragma unroll
     for (int c = 0; c < D; c++) a.ce[((u64)proof * D + c) * nce + i] = val.c(c);
 }
@@ -410,18 +412,36 @@ __global__ __launch_bounds__(256) void ood_kernel(const u64* coef, const u64* hc
     F acc[15];
 #pragma unroll
     for (int q = 0; q < 15; q++) acc[q] = F::zero();
-#pragma unroll 2
+    // the 8 (7 columns + H) values of index j + T are loaded before the products of index j run:
+    // a load next to its multiply would be waited for one at a time (the field primitives are asm
+    // statements the scheduler does not move loads across)
+    u64 cur[7], nxt[7];
+    F hc, hn;
+    {
+        const u64 j = base + t;
+#pragma unroll
+        for (int c = 0; c < 7; c++) cur[c] = co[(u64)c * n + j];
+        hc = fe_plane<D>(h, n, j);
+    }
+#pragma unroll
     for (int r = 0; r < OOD_R; r++) {
-        const u64 j = base + (u64)r * T + t;
+        if (r + 1 < OOD_R) {
+            const u64 j = base + (u64)(r + 1) * T + t;
+#pragma unroll
+            for (int c = 0; c < 7; c++) nxt[c] = co[(u64)c * n + j];
+            hn = fe_plane<D>(h, n, j);
+        }
 #pragma unroll
         for (int c = 0; c < 7; c++) {
-            u64 v = co[(u64)c * n + j];
-            acc[2 * c] = fe_add(acc[2 * c], fe_mulb(pz, v));
-            acc[2 * c + 1] = fe_add(acc[2 * c + 1], fe_mulb(pzg, v));
+            acc[2 * c] = fe_add(acc[2 * c], fe_mulb(pz, cur[c]));
+            acc[2 * c + 1] = fe_add(acc[2 * c + 1], fe_mulb(pzg, cur[c]));
         }
-        acc[14] = fe_add(acc[14], fe_mul(fe_plane<D>(h, n, j), pz));
+        acc[14] = fe_add(acc[14], fe_mul(hc, pz));
         pz = fe_mul(pz, zT);
         pzg = fe_mul(pzg, zgT);
+#pragma unroll
+        for (int c = 0; c < 7; c++) cur[c] = nxt[c];
+        hc = hn;
     }
     // wave reduction, then across the (up to 4) waves
     const int W = T < 64 ? T : 64;
