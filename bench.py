@@ -356,7 +356,7 @@ def main():
                          "valu": valu_roofline(pmc, lde_ms, WIDTH * per * n * BLOWUP),
                          "kernel": "trace LDE (ntt_pass_a<8,false,8,4> + ntt_pass_b<8,false,8,4>), 7 columns x "
                                    f"{per} proofs, {lde_ms:.3f} ms/launch-set, {lde_bytes} algorithmic B",
-                         # the same launch sets inside the timed pipelined steps (per 16-proof unit,
+                         # the same launch sets inside the timed pipelined steps (per XFG_UNIT-proof unit,
                          # sharing the GPU with the other lanes' kernels)
                          "in_pipeline": in_pipeline(pipe_ms, pipe_sets, pipe_polys, n)},
             "stage_ms_one_batch": prover_stage,
