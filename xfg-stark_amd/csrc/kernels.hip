@@ -733,6 +733,50 @@ void launch_fri_fold(const u64* vals, u64 val_stride, u64 comp_stride, bool cose
     XFG_CHECK_LAUNCH();
 }
 
+// ============================================================================ device transcript
+__device__ __forceinline__ Digest dev_merge_int(const Digest& seed, u64 v) {
+    uint32_t m[16];
+#pragma unroll
+    for (int i = 0; i < 8; i++) m[i] = seed.w[i];
+    m[8] = (uint32_t)v;
+    m[9] = (uint32_t)(v >> 32);
+#pragma unroll
+    for (int i = 10; i < 16; i++) m[i] = 0;
+    return b3_hash_block(m, 40);
+}
+// Coin::draw_e: the first 8 D digest bytes as D LE elements, retried while any is >= p
+__device__ __forceinline__ bool dev_draw_e(DevCoin& c, u64* out, int D) {
+    for (int i = 0; i < 1000; i++) {
+        const Digest v = dev_merge_int(c.seed, ++c.counter);
+        const u64 x = (u64)v.w[0] | ((u64)v.w[1] << 32), y = (u64)v.w[2] | ((u64)v.w[3] << 32);
+        if (x < P && (D == 1 || y < P)) {
+            out[0] = x;
+            out[1] = y;
+            return true;
+        }
+    }
+    return false;
+}
+__global__ void fri_alpha_kernel(DevCoin* coins, const Digest* nodes, u64 node_stride, u64* alpha7, int* fail,
+                                 int npoly, int D) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= npoly) return;
+    DevCoin c = coins[b];
+    c.seed = b3_merge(c.seed, nodes[(u64)b * node_stride + 1]);  // reseed: counter restarts
+    c.counter = 0;
+    u64 a[2] = {0, 0};
+    if (!dev_draw_e(c, a, D)) fail[b] = 1;
+    const u64 inv7 = 0x249249246DB6DB6EULL;  // 7^-1 mod p
+    for (int k = 0; k < D; k++) alpha7[(u64)b * D + k] = gl_mul(a[k], inv7);
+    coins[b] = c;
+}
+void launch_fri_alpha(DevCoin* coins, const Digest* nodes, u64 node_stride, u64* alpha7, int* fail, int npoly,
+                      int ext, hipStream_t s) {
+    hipLaunchKernelGGL(fri_alpha_kernel, dim3((npoly + 63) / 64), dim3(64), 0, s, coins, nodes, node_stride, alpha7,
+                       fail, npoly, ext);
+    XFG_CHECK_LAUNCH();
+}
+
 // ============================================================================ gathers
 __global__ void gather_u64_kernel(const u64* src, const u64* idx, u64* dst, u64 count) {
     u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;

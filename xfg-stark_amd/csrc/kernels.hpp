@@ -99,6 +99,19 @@ void launch_fri_fold(const u64* vals, u64 val_stride, u64 comp_stride, bool cose
                      u64 rows, int logD, const u64* alpha7, u64* out, u64 out_stride, const Tables& T, int npoly,
                      int ext, hipStream_t s);
 
+// ---- device-side Fiat-Shamir (winter-crypto DefaultRandomCoin<Blake3_256>, as host_common.hpp Coin)
+struct DevCoin {
+    Digest seed;
+    u64 counter;
+    u64 pad;
+};
+// FRI layer step of the transcript on the device, one thread per proof: reseed with the layer's
+// Merkle root (heap node 1 of the proof's tree, nodes + b * node_stride), draw alpha in E (retried
+// while >= p, at most 1000 times) and write alpha7 [B][D] = alpha * 7^-1; fail[b] = 1 when every
+// draw was rejected. The host replays the same steps from the roots afterwards.
+void launch_fri_alpha(DevCoin* coins, const Digest* nodes, u64 node_stride, u64* alpha7, int* fail, int npoly,
+                      int ext, hipStream_t s);
+
 // ---- openings ----
 void launch_gather_u64(const u64* src, const u64* idx, u64* dst, u64 count, hipStream_t s);
 void launch_gather_digest(const Digest* src, const u64* idx, Digest* dst, u64 count, hipStream_t s);

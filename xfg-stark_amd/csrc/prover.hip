@@ -276,13 +276,18 @@ struct Lane {
         rem, gidx, gval, dn2;
     DBuf<Digest> tnodes, hnodes, gdig;
     DBuf<DeepParams> dp;
+    DBuf<DevCoin> dcoin;  // device-side transcript (FRI rounds)
+    DBuf<int> dfail;
     std::vector<DBuf<u64>> flayer;
     std::vector<DBuf<Digest>> fnodes;
     // pinned host staging
     HBuf<Digest> h_roots, h_gd;
-    HBuf<u64> h_co, h_zp, h_ood, h_a7, h_rem, h_dn2, h_idx, h_gv;
+    HBuf<u64> h_co, h_zp, h_ood, h_rem, h_dn2, h_idx, h_gv;
     HBuf<AirConst> h_air;
     HBuf<DeepParams> h_dp;
+    HBuf<DevCoin> h_coin;
+    HBuf<Digest> h_froots;
+    HBuf<int> h_fail;
     // host scratch of the opening plans and the serialiser, kept across units so steady-state
     // units neither allocate nor page-fault (their cost grew with the shared hosts' load)
     struct {
@@ -292,9 +297,14 @@ struct Lane {
     } hs;
     void release() {
         for (auto* b : {&h_roots, &h_gd}) b->release();
-        for (auto* b : {&h_co, &h_zp, &h_ood, &h_a7, &h_rem, &h_dn2, &h_idx, &h_gv}) b->release();
+        for (auto* b : {&h_co, &h_zp, &h_ood, &h_rem, &h_dn2, &h_idx, &h_gv}) b->release();
         h_air.release();
         h_dp.release();
+        h_coin.release();
+        h_froots.release();
+        h_fail.release();
+        dcoin.release();
+        dfail.release();
         air.release();
         for (auto* b : {&coeffs, &trace, &coef, &scratch, &lde, &ce, &hcoef, &hlde, &zpts, &partial, &ood,
                         &carry, &deep, &f0, &alpha7, &rem, &gidx, &gval, &dn2})
@@ -670,8 +680,21 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     stage_mark(c, 7);
 
     // ---- 6. FRI layers (FriProver::build_layers), folding factor 8
-    u64* alpha7h = c->h_a7.ensure((size_t)B * DE);
-    const u64 inv7 = gl_inv(GEN);
+    // The commit -> reseed -> draw alpha -> fold rounds run as one chain of launches: the coin steps
+    // run on the device (launch_fri_alpha, from the coins as they stand after the DEEP draws), so
+    // no round needs a host round trip; the host replays the same steps from the layer roots below.
+    {
+        DevCoin* hc = c->h_coin.ensure(B);
+        for (int b = 0; b < B; b++) {
+            hc[b].seed = jobs[b].coin.seed;
+            hc[b].counter = jobs[b].coin.counter;
+            hc[b].pad = 0;
+        }
+        c->dcoin.ensure(B);
+        c->dfail.ensure(B);
+        HIPCHK(hipMemcpyAsync(c->dcoin.p, hc, B * sizeof(DevCoin), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemsetAsync(c->dfail.p, 0, B * sizeof(int), s));
+    }
     for (unsigned l = 0; l < nl; l++) {
         const u64 rows = D[l] / 8;
         const bool cm = (l == 0);
@@ -680,23 +703,17 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         u64 top = launch_fri_leaves(src, sstride, cstride, cm, logn, logbeta, rows, c->fnodes[l].p, 2 * rows, B, DE,
                                     s);
         launch_tree_top(c->fnodes[l].p, 2 * rows, top, B, s);
-        ht.mark("fri_launch");
-        fetch_roots(c, c->fnodes[l].p, 2 * rows, B, roots);
-        ht.mark("sync_fri");
-        for (int b = 0; b < B; b++) {
-            auto& j = jobs[b];
-            uint8_t rb[32];
-            digest_bytes(roots[b], rb);
-            j.commitments.insert(j.commitments.end(), rb, rb + 32);
-            j.coin.reseed(roots[b]);
-            u64 a[2] = {0, 0};
-            if (!j.coin.draw_e(a, DE)) j.status = XFG_PROVER_ERROR;
-            for (int k = 0; k < DE; k++) alpha7h[(size_t)b * DE + k] = gl_mul(a[k], inv7);
-        }
-        HIPCHK(hipMemcpyAsync(c->alpha7.p, alpha7h, (size_t)B * DE * 8, hipMemcpyHostToDevice, s));
+        launch_fri_alpha(c->dcoin.p, c->fnodes[l].p, 2 * rows, c->alpha7.p, c->dfail.p, B, DE, s);
         launch_fri_fold(src, sstride, cstride, cm, logn, logbeta, rows, (int)ilog2(D[l]), c->alpha7.p,
                         c->flayer[l + 1].p, rows, T, B, DE, s);
     }
+    ht.mark("fri_launch");
+    Digest* froots = c->h_froots.ensure((size_t)std::max(1u, nl) * B);
+    int* ffail = c->h_fail.ensure(B);
+    for (unsigned l = 0; l < nl; l++)
+        HIPCHK(hipMemcpy2DAsync(froots + (size_t)l * B, sizeof(Digest), c->fnodes[l].p + 1,
+                                2 * (D[l] / 8) * sizeof(Digest), sizeof(Digest), B, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(ffail, c->dfail.p, B * sizeof(int), hipMemcpyDeviceToHost, s));
     // remainder: interpolate the last layer over 7*<w_D>, keep D/blowup coefficients
     // (with no folding layer this is the DEEP polynomial's own coefficients)
     u64* remh = c->h_rem.ensure((size_t)B * DE * rem_len);  // planes [b][c][rem_len]
@@ -714,6 +731,23 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     ht.mark("launch_rem");
     HIPCHK(hipStreamSynchronize(s));
     ht.mark("sync_rem");
+    // host replay of the FRI rounds: layer commitments into the proof, the coin advanced exactly as
+    // the device coin was (the device's alpha draws must have failed exactly where these fail)
+    for (int b = 0; b < B; b++) {
+        auto& j = jobs[b];
+        bool failed = false;
+        for (unsigned l = 0; l < nl; l++) {
+            const Digest& r = froots[(size_t)l * B + b];
+            uint8_t rb[32];
+            digest_bytes(r, rb);
+            j.commitments.insert(j.commitments.end(), rb, rb + 32);
+            j.coin.reseed(r);
+            u64 a[2] = {0, 0};
+            if (!j.coin.draw_e(a, DE)) failed = true;
+        }
+        if (failed) j.status = XFG_PROVER_ERROR;
+        if (failed != (nl > 0 && ffail[b] != 0)) throw std::runtime_error("device / host FRI transcript diverged");
+    }
 
     auto t_q0 = std::chrono::steady_clock::now();
     // ---- 7. grinding + query positions, gather lists
