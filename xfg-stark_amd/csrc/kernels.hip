@@ -751,11 +751,167 @@ __device__ __forceinline__ bool dev_draw_e(DevCoin& c, u64* out, int D) {
         const u64 x = (u64)v.w[0] | ((u64)v.w[1] << 32), y = (u64)v.w[2] | ((u64)v.w[3] << 32);
         if (x < P && (D == 1 || y < P)) {
             out[0] = x;
-            out[1] = y;
+            out[1] = D == 2 ? y : 0;
             return true;
         }
     }
     return false;
+}
+__device__ __forceinline__ void dev_reseed(DevCoin& c, const Digest& d) {
+    c.seed = b3_merge(c.seed, d);
+    c.counter = 0;
+}
+// Blake3_256::hash_elements of cnt <= 128 elements: one chunk of ceil(8 cnt / 64) blocks
+__device__ Digest dev_hash_elems(const u64* e, int cnt) {
+    uint32_t cv[8] = {XFG_B3_IV0, XFG_B3_IV1, XFG_B3_IV2, XFG_B3_IV3, XFG_B3_IV4, XFG_B3_IV5, XFG_B3_IV6, XFG_B3_IV7};
+    const int len = 8 * cnt, nb = (len + 63) / 64;
+    Digest d;
+    for (int blk = 0; blk < nb; blk++) {
+        uint32_t m[16];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int k = 8 * blk + i;
+            const u64 v = k < cnt ? e[k] : 0;
+            m[2 * i] = (uint32_t)v;
+            m[2 * i + 1] = (uint32_t)(v >> 32);
+        }
+        const bool last = blk == nb - 1;
+        const uint32_t flags = (blk == 0 ? B3_CHUNK_START : 0u) | (last ? B3_CHUNK_END | B3_ROOT : 0u);
+        uint32_t out[8];
+        b3_compress(cv, m, last ? (uint32_t)(len - 64 * blk) : 64u, 0, flags, out);
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            cv[i] = out[i];
+            d.w[i] = out[i];
+        }
+    }
+    return d;
+}
+// k <= 64 consecutive draws of E by one full wave, every lane holding the same coin: lane i hashes
+// counter + 1 + i at once, and the accepted candidates in counter order are exactly the draws
+// Coin::draw_e makes one after another (a rejected candidate is the one its retry skips). Draw j
+// goes to out[j S .. j S + D) (S = stride >= D). If the window holds fewer than k accepted candidates (>= 50
+// rejections of probability 2^-32 each) the rest are drawn one at a time after the last accepted.
+// The latency is one compression instead of k: these draws sit between two launches of the chain.
+__device__ bool wave_draw_e(DevCoin& c, int k, int D, u64* out, int S) {
+    const int lane = threadIdx.x & 63;
+    const Digest v = dev_merge_int(c.seed, c.counter + 1 + lane);
+    const u64 x = (u64)v.w[0] | ((u64)v.w[1] << 32), y = (u64)v.w[2] | ((u64)v.w[3] << 32);
+    const bool ok = x < P && (D == 1 || y < P);
+    const u64 mask = __ballot(ok);
+    const int idx = __popcll(mask & ((1ULL << lane) - 1));
+    if (ok && idx < k) {
+        out[idx * S] = x;
+        if (D == 2) out[idx * S + 1] = y;
+    }
+    const int got = __popcll(mask);
+    if (got >= k) {
+        u64 m = mask;
+        for (int i = 1; i < k; i++) m &= m - 1;  // lowest set bit = the k-th accepted candidate
+        c.counter += __ffsll((unsigned long long)m);
+        return true;
+    }
+    if (got > 0) c.counter += 64 - __clzll(mask);  // just past the last accepted candidate
+    bool all = true;
+    for (int j = got; j < k; j++) {
+        u64 a[2] = {0, 0};
+        all &= dev_draw_e(c, a, D);
+        if (lane == 0)
+            for (int d = 0; d < D; d++) out[j * S + d] = a[d];
+    }
+    return all;
+}
+// winter-prover Prover::prove after the trace commitment: reseed(trace root), draw the 15 constraint
+// composition coefficients (7 transition, 8 boundary); one wave per proof
+__global__ __launch_bounds__(64) void coin_coeffs_kernel(DevCoin* coins, const Digest* nodes, u64 node_stride,
+                                                         u64* coeffs, int* fail, int D) {
+    const int b = blockIdx.x;
+    DevCoin c = coins[b];
+    dev_reseed(c, nodes[(u64)b * node_stride + 1]);
+    const bool ok = wave_draw_e(c, 15, D, coeffs + (u64)b * 15 * D, D);
+    if (threadIdx.x == 0) {
+        if (!ok) fail[b] = 1;
+        coins[b] = c;
+    }
+}
+__global__ void coin_ood_point_kernel(DevCoin* coins, const Digest* nodes, u64 node_stride, u64 g, u64* zpts,
+                                      int* fail, int npoly, int D) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= npoly) return;
+    DevCoin c = coins[b];
+    dev_reseed(c, nodes[(u64)b * node_stride + 1]);
+    u64 z[2] = {0, 0};
+    bool ok = dev_draw_e(c, z, D);
+    if (z[0] == 0 && z[1] == 0) ok = false;  // z = 0 (then z g = 0 too): no DEEP quotient
+    for (int k = 0; k < D; k++) {
+        zpts[(u64)b * 2 * D + k] = z[k];
+        zpts[(u64)b * 2 * D + D + k] = gl_mul(z[k], g);
+    }
+    if (!ok) fail[b] = 1;
+    coins[b] = c;
+}
+// DEEP coefficients, two waves per proof: wave 0 runs the transcript (two element hashes, the 8
+// draws), wave 1 meanwhile inverts z (1 / (z g) = (1 / z) g^-1: one inversion)
+__global__ __launch_bounds__(128) void coin_deep_kernel(DevCoin* coins, const u64* ood, const u64* zpts, u64 ginv,
+                                                        DeepParams* dp, int* fail, int D) {
+    __shared__ u64 ab[8][2];  // a_0..a_6, gamma
+    __shared__ E2 zinv;
+    __shared__ int ok_s;
+    const int b = blockIdx.x;
+    const u64* o = ood + (u64)b * 15 * D;  // [T_c(z), T_c(zg)] x 7, H(z): E elements, coordinates interleaved
+    const u64* zb = zpts + (u64)b * 2 * D;
+    const E2 z{zb[0], D == 2 ? zb[1] : 0}, zg{zb[D], D == 2 ? zb[D + 1] : 0};
+    const bool zz = z.a == 0 && z.b == 0;  // z g == 0 <=> z == 0
+    if (threadIdx.x < 64) {
+        DevCoin c = coins[b];
+        dev_reseed(c, dev_hash_elems(o, 14 * D));
+        dev_reseed(c, dev_hash_elems(o + 14 * D, D));
+        const bool ok = wave_draw_e(c, 8, D, &ab[0][0], 2);
+        if (threadIdx.x == 0) {
+            coins[b] = c;
+            ok_s = ok;
+        }
+    } else if (threadIdx.x == 64) {
+        zinv = zz ? E2{0, 0} : e2_inv(z);
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    DeepParams P = {};
+    for (int k = 0; k < 7; k++)
+        for (int d = 0; d < D; d++) P.a[k][d] = ab[k][d];
+    for (int d = 0; d < D; d++) P.gamma[d] = ab[7][d];
+    auto put = [](u64* d, E2 v) { d[0] = v.a; d[1] = v.b; };
+    auto ood_e = [&](int q) { return E2{o[q * D], D == 2 ? o[q * D + 1] : 0}; };
+    put(P.z, z);
+    put(P.zg, zg);
+    put(P.zinv, zinv);
+    put(P.zginv, e2_mulb(zinv, ginv));
+    E2 c1 = e2_mul(E2{P.gamma[0], P.gamma[1]}, ood_e(14)), c2{0, 0};
+    for (int k = 0; k < 7; k++) {
+        const E2 a{P.a[k][0], P.a[k][1]};
+        c1 = e2_add(c1, e2_mul(a, ood_e(2 * k)));
+        c2 = e2_add(c2, e2_mul(a, ood_e(2 * k + 1)));
+    }
+    put(P.c1, c1);
+    put(P.c2, c2);
+    dp[b] = P;
+    if (!ok_s || zz) fail[b] = 1;
+}
+void launch_coin_coeffs(DevCoin* coins, const Digest* nodes, u64 node_stride, u64* coeffs, int* fail, int npoly,
+                        int ext, hipStream_t s) {
+    hipLaunchKernelGGL(coin_coeffs_kernel, dim3(npoly), dim3(64), 0, s, coins, nodes, node_stride, coeffs, fail, ext);
+    XFG_CHECK_LAUNCH();
+}
+void launch_coin_ood_point(DevCoin* coins, const Digest* nodes, u64 node_stride, u64 g, u64* zpts, int* fail,
+                           int npoly, int ext, hipStream_t s) {
+    hipLaunchKernelGGL(coin_ood_point_kernel, dim3((npoly + 63) / 64), dim3(64), 0, s, coins, nodes, node_stride, g,
+                       zpts, fail, npoly, ext);
+    XFG_CHECK_LAUNCH();
+}
+void launch_coin_deep(DevCoin* coins, const u64* ood, const u64* zpts, u64 ginv, DeepParams* dp, int* fail, int npoly,
+                      int ext, hipStream_t s) {
+    hipLaunchKernelGGL(coin_deep_kernel, dim3(npoly), dim3(128), 0, s, coins, ood, zpts, ginv, dp, fail, ext);
+    XFG_CHECK_LAUNCH();
 }
 __global__ void fri_alpha_kernel(DevCoin* coins, const Digest* nodes, u64 node_stride, u64* alpha7, int* fail,
                                  int npoly, int D) {

@@ -111,6 +111,17 @@ struct DevCoin {
 // draw was rejected. The host replays the same steps from the roots afterwards.
 void launch_fri_alpha(DevCoin* coins, const Digest* nodes, u64 node_stride, u64* alpha7, int* fail, int npoly,
                       int ext, hipStream_t s);
+// the earlier transcript steps, same conventions (fail[b] = 1 on a rejected draw or a zero OOD point):
+// reseed with the trace root, draw the 15 composition coefficients -> coeffs [B][15][D]
+void launch_coin_coeffs(DevCoin* coins, const Digest* nodes, u64 node_stride, u64* coeffs, int* fail, int npoly,
+                        int ext, hipStream_t s);
+// reseed with the composition root, draw z -> zpts [B][2][D] = (z, z g)
+void launch_coin_ood_point(DevCoin* coins, const Digest* nodes, u64 node_stride, u64 g, u64* zpts, int* fail,
+                           int npoly, int ext, hipStream_t s);
+// reseed with hash(trace OOD frame), hash(H(z)) (ood [B][15][D]), draw a_0..a_6, gamma -> dp [B]
+// (ginv = g^-1, the trace domain generator's inverse)
+void launch_coin_deep(DevCoin* coins, const u64* ood, const u64* zpts, u64 ginv, DeepParams* dp, int* fail, int npoly,
+                      int ext, hipStream_t s);
 
 // ---- openings ----
 void launch_gather_u64(const u64* src, const u64* idx, u64* dst, u64 count, hipStream_t s);

@@ -282,10 +282,10 @@ struct Lane {
     std::vector<DBuf<Digest>> fnodes;
     // pinned host staging
     HBuf<Digest> h_roots, h_gd;
-    HBuf<u64> h_co, h_zp, h_ood, h_rem, h_dn2, h_idx, h_gv;
+    HBuf<u64> h_co, h_ood, h_rem, h_dn2, h_idx, h_gv;
     HBuf<AirConst> h_air;
-    HBuf<DeepParams> h_dp;
     HBuf<DevCoin> h_coin;
+    HBuf<DeepParams> h_dp;
     HBuf<Digest> h_froots;
     HBuf<int> h_fail;
     // host scratch of the opening plans and the serialiser, kept across units so steady-state
@@ -297,10 +297,10 @@ struct Lane {
     } hs;
     void release() {
         for (auto* b : {&h_roots, &h_gd}) b->release();
-        for (auto* b : {&h_co, &h_zp, &h_ood, &h_rem, &h_dn2, &h_idx, &h_gv}) b->release();
+        for (auto* b : {&h_co, &h_ood, &h_rem, &h_dn2, &h_idx, &h_gv}) b->release();
         h_air.release();
-        h_dp.release();
         h_coin.release();
+        h_dp.release();
         h_froots.release();
         h_fail.release();
         dcoin.release();
@@ -425,13 +425,6 @@ static void ensure_fourstep(xfg_ctx* c, int logn, int logbeta) {
     for (int l = 3; l <= std::min(logn + 1, FOURSTEP_MAX_LOG); l++)
         if (!f.inv[l]) f.inv[l] = build(l, -1);
     HIPCHK(hipStreamSynchronize(0));
-}
-
-// D2H of the root (heap index 1) of B trees laid out with a per-proof stride
-static void fetch_roots(Lane* c, const Digest* nodes, u64 stride, int B, Digest* out) {
-    HIPCHK(hipMemcpy2DAsync(out, sizeof(Digest), nodes + 1, stride * sizeof(Digest), sizeof(Digest), B,
-                            hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
 }
 
 struct ProofJob {
@@ -564,6 +557,22 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         j.coin.init(e, 20);
         j.commitments.clear();
     }
+    // The Fiat-Shamir steps between the commitments (coefficient, OOD point, DEEP and FRI alpha
+    // draws) run on the device from a copy of each proof's coin, so the whole chain from the trace
+    // to the FRI remainder is enqueued without a host round trip; the host replays the same
+    // transcript from the roots and OOD values once the chain has finished (below).
+    {
+        DevCoin* hc = c->h_coin.ensure(B);
+        for (int b = 0; b < B; b++) {
+            hc[b].seed = jobs[b].coin.seed;
+            hc[b].counter = jobs[b].coin.counter;
+            hc[b].pad = 0;
+        }
+        c->dcoin.ensure(B);
+        c->dfail.ensure(B);
+        HIPCHK(hipMemcpyAsync(c->dcoin.p, hc, B * sizeof(DevCoin), hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemsetAsync(c->dfail.p, 0, B * sizeof(int), s));
+    }
 
     // ---- 1. trace LDE + commitment (DefaultTraceLde::new)
     ht.mark("setup");
@@ -584,24 +593,10 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     stage_mark(c, 1);
     launch_tree_top(c->tnodes.p, 2 * n, launch_leaves_lde(c->lde.p, 7, c->tnodes.p, 2 * n, B, logn, logbeta, s), B,
                     s);
-    Digest* roots = c->h_roots.ensure(B);
     stage_mark(c, 2);
-    ht.mark("launch1");
-    fetch_roots(c, c->tnodes.p, 2 * n, B, roots);
-    ht.mark("sync_trace_root");
 
     // ---- 2. constraint composition coefficients (7 transition + 8 boundary)
-    u64* co = c->h_co.ensure((size_t)B * 15 * DE);
-    for (int b = 0; b < B; b++) {
-        auto& j = jobs[b];
-        uint8_t rb[32];
-        digest_bytes(roots[b], rb);
-        j.commitments.insert(j.commitments.end(), rb, rb + 32);
-        j.coin.reseed(roots[b]);
-        for (int k = 0; k < 15; k++)
-            if (!j.coin.draw_e(co + ((size_t)b * 15 + k) * DE, DE)) j.status = XFG_PROVER_ERROR;
-    }
-    HIPCHK(hipMemcpyAsync(c->coeffs.p, co, (size_t)B * 15 * DE * 8, hipMemcpyHostToDevice, s));
+    launch_coin_coeffs(c->dcoin.p, c->tnodes.p, 2 * n, c->coeffs.p, c->dfail.p, B, DE, s);
 
     // ---- 3. constraint evaluation + composition polynomial + commitment
     launch_constraint_eval(c->lde.p, c->air.p, c->coeffs.p, ce_div, c->ce.p, logn, logbeta, B, DE, s);
@@ -612,89 +607,22 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     launch_tree_top(c->hnodes.p, 2 * n, launch_leaves_lde(c->hlde.p, DE, c->hnodes.p, 2 * n, B, logn, logbeta, s), B,
                     s);
     stage_mark(c, 5);
-    ht.mark("launch2");
-    fetch_roots(c, c->hnodes.p, 2 * n, B, roots);
-    ht.mark("sync_comp_root");
 
-    // ---- 4. OOD point and frame
-    const u64 g = gl_root(logn);
-    u64* zp = c->h_zp.ensure((size_t)B * 2 * DE);  // [b][z, z g][DE]
-    for (int b = 0; b < B; b++) {
-        auto& j = jobs[b];
-        uint8_t rb[32];
-        digest_bytes(roots[b], rb);
-        j.commitments.insert(j.commitments.end(), rb, rb + 32);
-        j.coin.reseed(roots[b]);
-        u64 z[2] = {0, 0};
-        if (!j.coin.draw_e(z, DE)) j.status = XFG_PROVER_ERROR;
-        for (int k = 0; k < DE; k++) {
-            zp[(size_t)b * 2 * DE + k] = z[k];
-            zp[(size_t)b * 2 * DE + DE + k] = gl_mul(z[k], g);
-        }
-    }
-    HIPCHK(hipMemcpyAsync(c->zpts.p, zp, (size_t)B * 2 * DE * 8, hipMemcpyHostToDevice, s));
+    // ---- 4. OOD point (z, z g) and frame
+    launch_coin_ood_point(c->dcoin.p, c->hnodes.p, 2 * n, gl_root(logn), c->zpts.p, c->dfail.p, B, DE, s);
     launch_ood(c->coef.p, c->hcoef.p, c->zpts.p, c->partial.p, c->ood.p, logn, B, DE, s);
-    u64* ood = c->h_ood.ensure((size_t)B * 15 * DE);
-    HIPCHK(hipMemcpyAsync(ood, c->ood.p, (size_t)B * 15 * DE * 8, hipMemcpyDeviceToHost, s));
     stage_mark(c, 6);
-    ht.mark("launch3");
-    HIPCHK(hipStreamSynchronize(s));
-    ht.mark("sync_ood");
 
     // ---- 5. DEEP composition polynomial (coefficient form) + its LDE
-    DeepParams* dps = c->h_dp.ensure(B);
-    for (int b = 0; b < B; b++) {
-        auto& j = jobs[b];
-        memcpy(j.ood, &ood[(size_t)b * 15 * DE], 15 * DE * 8);  // [15][DE]
-        j.coin.reseed(hash_elements(j.ood, 14 * DE));  // interleaved T_i(z), T_i(zg), E elements
-        j.coin.reseed(hash_elements(j.ood + 14 * DE, DE));
-        DeepParams& P = dps[b];
-        memset(&P, 0, sizeof P);
-        for (int k = 0; k < 7; k++)
-            if (!j.coin.draw_e(P.a[k], DE)) j.status = XFG_PROVER_ERROR;
-        if (!j.coin.draw_e(P.gamma, DE)) j.status = XFG_PROVER_ERROR;
-        const u64* zb = zp + (size_t)b * 2 * DE;
-        const E2 z{zb[0], DE == 2 ? zb[1] : 0}, zg{zb[DE], DE == 2 ? zb[DE + 1] : 0};
-        if ((z.a == 0 && z.b == 0) || (zg.a == 0 && zg.b == 0)) j.status = XFG_PROVER_ERROR;
-        const E2 zi = (z.a || z.b) ? e2_inv(z) : E2{0, 0}, zgi = (zg.a || zg.b) ? e2_inv(zg) : E2{0, 0};
-        auto put = [](u64* d, E2 v) { d[0] = v.a; d[1] = v.b; };
-        auto ood_e = [&](int q) { return E2{j.ood[q * DE], DE == 2 ? j.ood[q * DE + 1] : 0}; };
-        put(P.z, z);
-        put(P.zg, zg);
-        put(P.zinv, zi);
-        put(P.zginv, zgi);
-        E2 c1 = e2_mul(E2{P.gamma[0], P.gamma[1]}, ood_e(14)), c2{0, 0};
-        for (int k = 0; k < 7; k++) {
-            const E2 a{P.a[k][0], P.a[k][1]};
-            c1 = e2_add(c1, e2_mul(a, ood_e(2 * k)));
-            c2 = e2_add(c2, e2_mul(a, ood_e(2 * k + 1)));
-        }
-        put(P.c1, c1);
-        put(P.c2, c2);
-    }
-    HIPCHK(hipMemcpyAsync(c->dp.p, dps, B * sizeof(DeepParams), hipMemcpyHostToDevice, s));
+    launch_coin_deep(c->dcoin.p, c->ood.p, c->zpts.p, gl_inv(gl_root(logn)), c->dp.p, c->dfail.p, B, DE, s);
     launch_deep(c->coef.p, c->hcoef.p, c->dp.p, c->partial.p, c->carry.p, c->deep.p, logn, B, DE, s);
     launch_lde(c->deep.p, n, c->f0.p, c->scratch.p, B * DE, logn, logbeta, T, s);
     // degree check: deg(DEEP) == n - 2  <=>  coefficient n-2 != 0 (coefficient n-1 is 0 by construction)
     HIPCHK(hipMemcpy2DAsync(c->dn2.p, 8, c->deep.p + (n - 2), n * 8, 8, (size_t)B * DE, hipMemcpyDeviceToDevice, s));
     stage_mark(c, 7);
 
-    // ---- 6. FRI layers (FriProver::build_layers), folding factor 8
-    // The commit -> reseed -> draw alpha -> fold rounds run as one chain of launches: the coin steps
-    // run on the device (launch_fri_alpha, from the coins as they stand after the DEEP draws), so
-    // no round needs a host round trip; the host replays the same steps from the layer roots below.
-    {
-        DevCoin* hc = c->h_coin.ensure(B);
-        for (int b = 0; b < B; b++) {
-            hc[b].seed = jobs[b].coin.seed;
-            hc[b].counter = jobs[b].coin.counter;
-            hc[b].pad = 0;
-        }
-        c->dcoin.ensure(B);
-        c->dfail.ensure(B);
-        HIPCHK(hipMemcpyAsync(c->dcoin.p, hc, B * sizeof(DevCoin), hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemsetAsync(c->dfail.p, 0, B * sizeof(int), s));
-    }
+    // ---- 6. FRI layers (FriProver::build_layers), folding factor 8: commit -> reseed -> draw alpha
+    // -> fold, every round on the device
     for (unsigned l = 0; l < nl; l++) {
         const u64 rows = D[l] / 8;
         const bool cm = (l == 0);
@@ -707,7 +635,19 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         launch_fri_fold(src, sstride, cstride, cm, logn, logbeta, rows, (int)ilog2(D[l]), c->alpha7.p,
                         c->flayer[l + 1].p, rows, T, B, DE, s);
     }
-    ht.mark("fri_launch");
+    ht.mark("chain_launch");
+    // transcript inputs for the host replay: trace / composition roots, OOD frame, FRI roots
+    Digest* roots = c->h_roots.ensure((size_t)2 * B);
+    HIPCHK(hipMemcpy2DAsync(roots, sizeof(Digest), c->tnodes.p + 1, 2 * n * sizeof(Digest), sizeof(Digest), B,
+                            hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpy2DAsync(roots + B, sizeof(Digest), c->hnodes.p + 1, 2 * n * sizeof(Digest), sizeof(Digest), B,
+                            hipMemcpyDeviceToHost, s));
+    u64* ood = c->h_ood.ensure((size_t)B * 15 * DE);
+    HIPCHK(hipMemcpyAsync(ood, c->ood.p, (size_t)B * 15 * DE * 8, hipMemcpyDeviceToHost, s));
+    u64* co = c->h_co.ensure((size_t)B * 15 * DE);  // the device's draws, checked by the replay
+    HIPCHK(hipMemcpyAsync(co, c->coeffs.p, (size_t)B * 15 * DE * 8, hipMemcpyDeviceToHost, s));
+    DeepParams* dps = c->h_dp.ensure(B);
+    HIPCHK(hipMemcpyAsync(dps, c->dp.p, B * sizeof(DeepParams), hipMemcpyDeviceToHost, s));
     Digest* froots = c->h_froots.ensure((size_t)std::max(1u, nl) * B);
     int* ffail = c->h_fail.ensure(B);
     for (unsigned l = 0; l < nl; l++)
@@ -731,22 +671,39 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     ht.mark("launch_rem");
     HIPCHK(hipStreamSynchronize(s));
     ht.mark("sync_rem");
-    // host replay of the FRI rounds: layer commitments into the proof, the coin advanced exactly as
-    // the device coin was (the device's alpha draws must have failed exactly where these fail)
+    // host replay of the transcript: commitments into the proof and the coin advanced exactly as the
+    // device coin was; the device's coefficient, z and DEEP draws (and its rejections) must agree
     for (int b = 0; b < B; b++) {
         auto& j = jobs[b];
-        bool failed = false;
-        for (unsigned l = 0; l < nl; l++) {
-            const Digest& r = froots[(size_t)l * B + b];
+        bool failed = false, same = true;
+        auto commit = [&](const Digest& r) {
             uint8_t rb[32];
             digest_bytes(r, rb);
             j.commitments.insert(j.commitments.end(), rb, rb + 32);
             j.coin.reseed(r);
+        };
+        auto draw = [&](const u64* dev) {  // dev: the device's value (DE coordinates) or null
             u64 a[2] = {0, 0};
             if (!j.coin.draw_e(a, DE)) failed = true;
+            for (int d = 0; dev && d < DE; d++) same &= a[d] == dev[d];
+            return a[0] | a[1];
+        };
+        const DeepParams& P = dps[b];
+        commit(roots[b]);
+        for (int k = 0; k < 15; k++) draw(co + ((size_t)b * 15 + k) * DE);  // composition coefficients
+        commit(roots[B + b]);
+        if (draw(P.z) == 0) failed = true;  // z = 0: no DEEP quotient
+        memcpy(j.ood, &ood[(size_t)b * 15 * DE], 15 * DE * 8);  // [15][DE]
+        j.coin.reseed(hash_elements(j.ood, 14 * DE));  // interleaved T_i(z), T_i(zg), E elements
+        j.coin.reseed(hash_elements(j.ood + 14 * DE, DE));
+        for (int k = 0; k < 7; k++) draw(P.a[k]);
+        draw(P.gamma);
+        for (unsigned l = 0; l < nl; l++) {
+            commit(froots[(size_t)l * B + b]);
+            draw(nullptr);  // FRI alpha
         }
         if (failed) j.status = XFG_PROVER_ERROR;
-        if (failed != (nl > 0 && ffail[b] != 0)) throw std::runtime_error("device / host FRI transcript diverged");
+        if (failed != (ffail[b] != 0) || !same) throw std::runtime_error("device / host transcript diverged");
     }
 
     auto t_q0 = std::chrono::steady_clock::now();
