@@ -1024,11 +1024,12 @@ static int max_lanes() {
     static const int v = std::max(1, env_int("XFG_LANES", 7));
     return v;
 }
-// 20 proofs per unit: a 64-proof batch becomes 20 + 20 + 20 + 4, and the uneven units keep the
-// lanes from running their latency-bound FRI / opening phases in lockstep (same box, 4 x 30 steps:
-// 10,680 +- 136 burn-proofs/s against 10,378 +- 181 with 16 and 10,592 +- 125 with 24)
+// 22 proofs per unit: a 64-proof batch becomes 22 + 22 + 20. Same box, 3 x 40 steps, with the unit's
+// transcript on the device: 11,400 +- 58 burn-proofs/s against 11,075 +- 103 with 20 (20 + 20 + 20 + 4),
+// 11,407 with 24, 11,302 with 23, 11,254-11,269 with 26-28, 10,790 with 32, 10,925 with 16.
+// (With host round trips between the stages 20 had been best: 10,680 against 10,592 with 24.)
 static int unit_size() {
-    static const int v = std::max(1, env_int("XFG_UNIT", 20));
+    static const int v = std::max(1, env_int("XFG_UNIT", 22));
     return v;
 }
 
