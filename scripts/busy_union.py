@@ -3,7 +3,7 @@ trace (default: the middle 60 % of the span of the named kernel's launches)"""
 import csv, glob, sys
 
 f = glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True)[0]
-key = sys.argv[2] if len(sys.argv) > 2 else "ntt_pass_a<8, false, 8, 4>"
+key = sys.argv[2] if len(sys.argv) > 2 else "ntt_pass_a_cos<8>"
 rows = list(csv.DictReader(open(f)))
 iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
 marks = [s for s, e, k in iv if key in k]

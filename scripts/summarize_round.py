@@ -6,8 +6,10 @@ import csv, glob, json, os, sys
 from collections import defaultdict
 
 out = sys.argv[1]
-PA, PB = "void xfg::ntt_pass_a<8, false, 8, 4>(xfg::NttArgs)", "void xfg::ntt_pass_b<8, false, 8, 4>(xfg::NttArgs)"
-LDE_GRID_A = 14680064  # grid of pass A for 7 columns x 64 proofs x 8 cosets (n = 2^16)
+PA, PB = "void xfg::ntt_pass_a_cos<8>(xfg::NttArgs)", "void xfg::ntt_pass_b<8, false, 8, 4>(xfg::NttArgs)"
+# grids (threads) of the trace-LDE launch set, 7 columns x 64 proofs at n = 2^16: pass A one block per
+# (16-column tile, column) covering all 8 cosets, pass B one thread per 16 outputs
+GRID = {PA: 16 * 448 * 256, PB: 14680064}
 
 def rows(pattern):
     f = glob.glob(os.path.join(out, pattern), recursive=True)
@@ -19,8 +21,8 @@ res = {"bench_value": bench["value"], "bench_ms_per_step": bench["ms_per_step"],
 tr = rows("trace/**/*kernel_trace.csv")
 grid = lambda r: int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
 ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], grid(r)) for r in tr)
-a = [e for e in ev if e[2] == PA and e[3] == LDE_GRID_A]
-b = [e for e in ev if e[2] == PB and e[3] == LDE_GRID_A]
+a = [e for e in ev if e[2] == PA and e[3] == GRID[PA]]
+b = [e for e in ev if e[2] == PB and e[3] == GRID[PB]]
 k = min(10, len(a), len(b))
 if k:
     da = sum(e[1] - e[0] for e in a[-k:]) / k / 1e6
@@ -31,7 +33,7 @@ if k:
 acc = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(os.path.join(out, "pmc*/**/*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
-        if int(r["Grid_Size"]) == LDE_GRID_A:
+        if GRID.get(r["Kernel_Name"]) == int(r["Grid_Size"]):
             acc[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
 mean = lambda v: sum(v) / len(v) if v else 0.0
 if PA in acc and PB in acc:
