@@ -29,6 +29,128 @@ __device__ __forceinline__ u64 tw_ipow(const Tables& T, int k, u64 e) {
     return T.tw[(M - ((e << (T.LM - k)) & (M - 1))) & (M - 1)];
 }
 
+// ============================================================================ device transcript
+// winter-crypto DefaultRandomCoin<Blake3_256> on the device (host twin: host_common.hpp Coin). The
+// transcript steps run inside the kernels that produce their inputs: the coefficient, OOD-point and
+// FRI alpha draws in the block that computes the Merkle root (tree_top_kernel), the DEEP draws in the
+// block that finishes the OOD sums (ood_final_kernel).
+__device__ __forceinline__ Digest dev_merge_int(const Digest& seed, u64 v) {
+    uint32_t m[16];
+#pragma unroll
+    for (int i = 0; i < 8; i++) m[i] = seed.w[i];
+    m[8] = (uint32_t)v;
+    m[9] = (uint32_t)(v >> 32);
+#pragma unroll
+    for (int i = 10; i < 16; i++) m[i] = 0;
+    return b3_hash_block(m, 40);
+}
+// Coin::draw_e: the first 8 D digest bytes as D LE elements, retried while any is >= p
+__device__ __forceinline__ bool dev_draw_e(DevCoin& c, u64* out, int D) {
+    for (int i = 0; i < 1000; i++) {
+        const Digest v = dev_merge_int(c.seed, ++c.counter);
+        const u64 x = (u64)v.w[0] | ((u64)v.w[1] << 32), y = (u64)v.w[2] | ((u64)v.w[3] << 32);
+        if (x < P && (D == 1 || y < P)) {
+            out[0] = x;
+            out[1] = D == 2 ? y : 0;
+            return true;
+        }
+    }
+    return false;
+}
+__device__ __forceinline__ void dev_reseed(DevCoin& c, const Digest& d) {
+    c.seed = b3_merge(c.seed, d);
+    c.counter = 0;
+}
+// Blake3_256::hash_elements of cnt <= 128 elements: one chunk of ceil(8 cnt / 64) blocks
+__device__ Digest dev_hash_elems(const u64* e, int cnt) {
+    uint32_t cv[8] = {XFG_B3_IV0, XFG_B3_IV1, XFG_B3_IV2, XFG_B3_IV3, XFG_B3_IV4, XFG_B3_IV5, XFG_B3_IV6, XFG_B3_IV7};
+    const int len = 8 * cnt, nb = (len + 63) / 64;
+    Digest d;
+    for (int blk = 0; blk < nb; blk++) {
+        uint32_t m[16];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int k = 8 * blk + i;
+            const u64 v = k < cnt ? e[k] : 0;
+            m[2 * i] = (uint32_t)v;
+            m[2 * i + 1] = (uint32_t)(v >> 32);
+        }
+        const bool last = blk == nb - 1;
+        const uint32_t flags = (blk == 0 ? B3_CHUNK_START : 0u) | (last ? B3_CHUNK_END | B3_ROOT : 0u);
+        uint32_t out[8];
+        b3_compress(cv, m, last ? (uint32_t)(len - 64 * blk) : 64u, 0, flags, out);
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            cv[i] = out[i];
+            d.w[i] = out[i];
+        }
+    }
+    return d;
+}
+// k <= 64 consecutive draws of E by one full wave, every lane holding the same coin: lane i hashes
+// counter + 1 + i at once, and the accepted candidates in counter order are exactly the draws
+// Coin::draw_e makes one after another (a rejected candidate is the one its retry skips). Draw j
+// goes to out[j S .. j S + D) (S = stride >= D). If the window holds fewer than k accepted candidates (>= 50
+// rejections of probability 2^-32 each) the rest are drawn one at a time after the last accepted.
+// The latency is one compression instead of k: these draws sit between two launches of the chain.
+__device__ bool wave_draw_e(DevCoin& c, int k, int D, u64* out, int S) {
+    const int lane = threadIdx.x & 63;
+    const Digest v = dev_merge_int(c.seed, c.counter + 1 + lane);
+    const u64 x = (u64)v.w[0] | ((u64)v.w[1] << 32), y = (u64)v.w[2] | ((u64)v.w[3] << 32);
+    const bool ok = x < P && (D == 1 || y < P);
+    const u64 mask = __ballot(ok);
+    const int idx = __popcll(mask & ((1ULL << lane) - 1));
+    if (ok && idx < k) {
+        out[idx * S] = x;
+        if (D == 2) out[idx * S + 1] = y;
+    }
+    const int got = __popcll(mask);
+    if (got >= k) {
+        u64 m = mask;
+        for (int i = 1; i < k; i++) m &= m - 1;  // lowest set bit = the k-th accepted candidate
+        c.counter += __ffsll((unsigned long long)m);
+        return true;
+    }
+    if (got > 0) c.counter += 64 - __clzll(mask);  // just past the last accepted candidate
+    bool all = true;
+    for (int j = got; j < k; j++) {
+        u64 a[2] = {0, 0};
+        all &= dev_draw_e(c, a, D);
+        if (lane == 0)
+            for (int d = 0; d < D; d++) out[j * S + d] = a[d];
+    }
+    return all;
+}
+// one wave (all lanes, uniform) of the block that computed proof b's root: reseed with the root,
+// then the draws that follow that commitment in Prover::prove
+__device__ void coin_root_step(const CoinStep& cs, int b, const Digest& root) {
+    const int D = cs.ext, lane = threadIdx.x;
+    DevCoin c = cs.coins[b];
+    dev_reseed(c, root);
+    bool ok;
+    if (cs.kind == CoinStep::COEFFS) {  // 7 transition + 8 boundary composition coefficients
+        ok = wave_draw_e(c, 15, D, cs.out + (u64)b * 15 * D, D);
+    } else {
+        u64 a[2] = {0, 0};
+        ok = dev_draw_e(c, a, D);
+        if (cs.kind == CoinStep::OOD_POINT) {  // z, and z g; z = 0 leaves no DEEP quotient
+            if (a[0] == 0 && a[1] == 0) ok = false;
+            if (lane == 0)
+                for (int k = 0; k < D; k++) {
+                    cs.out[(u64)b * 2 * D + k] = a[k];
+                    cs.out[(u64)b * 2 * D + D + k] = gl_mul(a[k], cs.g);
+                }
+        } else if (lane == 0) {  // FRI layer alpha, stored as alpha * 7^-1 for the fold
+            const u64 inv7 = 0x249249246DB6DB6EULL;
+            for (int k = 0; k < D; k++) cs.out[(u64)b * D + k] = gl_mul(a[k], inv7);
+        }
+    }
+    if (lane == 0) {
+        if (!ok) cs.fail[b] = 1;
+        cs.coins[b] = c;
+    }
+}
+
 // ============================================================================ Merkle
 // Heap layout per tree: nodes[1] = root, nodes[i] = H(nodes[2i] || nodes[2i+1]), leaf k at L + k
 // (MerkleTree::new / build_merkle_nodes, winter-crypto 0.8.3). For the LDE commitments only the
@@ -169,8 +291,8 @@ void launch_open_rows(const u64* lde, int nc, const u64* entries, u64 count, Dig
     XFG_CHECK_LAUNCH();
 }
 
-// last levels (count <= 512): one block per tree, LDS
-__global__ __launch_bounds__(256) void tree_top_kernel(Digest* nodes_all, u64 node_stride, u64 count) {
+// last levels (count <= 512): one block per tree, LDS; then the transcript step `cs` on the root
+__global__ __launch_bounds__(256) void tree_top_kernel(Digest* nodes_all, u64 node_stride, u64 count, CoinStep cs) {
     __shared__ Digest lds[256];
     Digest* nodes = nodes_all + (u64)blockIdx.x * node_stride;
     const int tid = threadIdx.x;
@@ -188,6 +310,7 @@ __global__ __launch_bounds__(256) void tree_top_kernel(Digest* nodes_all, u64 no
         }
         __syncthreads();
     }
+    if (cs.kind != CoinStep::NONE && tid < 64) coin_root_step(cs, blockIdx.x, count > 1 ? lds[0] : nodes[1]);
 }
 // middle levels: a block merges 512 consecutive nodes of level `count` (two per thread, coalesced)
 // and continues through LDS down to one node, writing every parent: count / 512 nodes remain
@@ -199,17 +322,17 @@ __global__ __launch_bounds__(256) void tree_mid_kernel(Digest* nodes_all, u64 no
     nodes[count / 2 + i] = d;
     block_tree_up(d, nodes, count / 2, lds, 1);
 }
-void launch_tree_top(Digest* nodes, u64 node_stride, u64 count, int npoly, hipStream_t s) {
+void launch_tree_top(Digest* nodes, u64 node_stride, u64 count, int npoly, hipStream_t s, const CoinStep& cs) {
     // one launch per 9 levels instead of one per level
     while (count > 512) {
         hipLaunchKernelGGL(tree_mid_kernel, dim3((unsigned)(count / 512), npoly), dim3(256), 0, s, nodes, node_stride,
                            count);
         count /= 512;
     }
-    if (count > 1) {
+    if (count > 1 || cs.kind != CoinStep::NONE) {
         int threads = (int)(count / 2);
         threads = threads < 64 ? 64 : threads;
-        hipLaunchKernelGGL(tree_top_kernel, dim3(npoly), dim3(threads), 0, s, nodes, node_stride, count);
+        hipLaunchKernelGGL(tree_top_kernel, dim3(npoly), dim3(threads), 0, s, nodes, node_stride, count, cs);
     }
     XFG_CHECK_LAUNCH();
 }
@@ -464,22 +587,74 @@ __global__ __launch_bounds__(256) void ood_kernel(const u64* coef, const u64* hc
         partial[((u64)proof * gridDim.x + blockIdx.x) * 15 * D + qc] = v;
     }
 }
-__global__ void ood_final_kernel(const u64* partial, int nblk, int d, u64* ood) {
+// DEEP coefficients (Prover::prove after the OOD frame), 128 threads for proof b with the frame o[15 D]
+// in LDS: wave 0 runs the transcript (reseed with the two element hashes, the 8 draws), wave 1
+// meanwhile inverts z (1 / (z g) = (1 / z) g^-1: one inversion)
+__device__ void deep_coin_block(const DeepCoinStep& dc, int b, const u64* o, int D) {
+    __shared__ u64 ab[8][2];  // a_0..a_6, gamma
+    __shared__ E2 zinv;
+    __shared__ int ok_s;
+    const u64* zb = dc.zpts + (u64)b * 2 * D;
+    const E2 z{zb[0], D == 2 ? zb[1] : 0}, zg{zb[D], D == 2 ? zb[D + 1] : 0};
+    const bool zz = z.a == 0 && z.b == 0;  // z g == 0 <=> z == 0
+    if (threadIdx.x < 64) {
+        DevCoin c = dc.coins[b];
+        dev_reseed(c, dev_hash_elems(o, 14 * D));  // [T_c(z), T_c(zg)] x 7, coordinates interleaved
+        dev_reseed(c, dev_hash_elems(o + 14 * D, D));  // H(z)
+        const bool ok = wave_draw_e(c, 8, D, &ab[0][0], 2);
+        if (threadIdx.x == 0) {
+            dc.coins[b] = c;
+            ok_s = ok;
+        }
+    } else if (threadIdx.x == 64) {
+        zinv = zz ? E2{0, 0} : e2_inv(z);
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    DeepParams P = {};
+    for (int k = 0; k < 7; k++)
+        for (int d = 0; d < D; d++) P.a[k][d] = ab[k][d];
+    for (int d = 0; d < D; d++) P.gamma[d] = ab[7][d];
+    auto put = [](u64* d, E2 v) { d[0] = v.a; d[1] = v.b; };
+    auto ood_e = [&](int q) { return E2{o[q * D], D == 2 ? o[q * D + 1] : 0}; };
+    put(P.z, z);
+    put(P.zg, zg);
+    put(P.zinv, zinv);
+    put(P.zginv, e2_mulb(zinv, dc.ginv));
+    E2 c1 = e2_mul(E2{P.gamma[0], P.gamma[1]}, ood_e(14)), c2{0, 0};
+    for (int k = 0; k < 7; k++) {
+        const E2 a{P.a[k][0], P.a[k][1]};
+        c1 = e2_add(c1, e2_mul(a, ood_e(2 * k)));
+        c2 = e2_add(c2, e2_mul(a, ood_e(2 * k + 1)));
+    }
+    put(P.c1, c1);
+    put(P.c2, c2);
+    dc.dp[b] = P;
+    if (!ok_s || zz) dc.fail[b] = 1;
+}
+// OOD block partials -> the frame ood[proof][15][D]; then the DEEP draws when dc.coins is set
+__global__ __launch_bounds__(128) void ood_final_kernel(const u64* partial, int nblk, int d, u64* ood, DeepCoinStep dc) {
+    __shared__ u64 o[30];
     const int proof = blockIdx.x, q = threadIdx.x;
-    if (q >= 15 * d) return;
-    u64 s = 0;
-    for (int b = 0; b < nblk; b++) s = gl_add(s, partial[((u64)proof * nblk + b) * 15 * d + q]);
-    ood[(u64)proof * 15 * d + q] = s;
+    if (q < 15 * d) {
+        u64 s = 0;
+        for (int b = 0; b < nblk; b++) s = gl_add(s, partial[((u64)proof * nblk + b) * 15 * d + q]);
+        ood[(u64)proof * 15 * d + q] = s;
+        o[q] = s;
+    }
+    if (!dc.coins) return;
+    __syncthreads();
+    deep_coin_block(dc, proof, o, d);
 }
 void launch_ood(const u64* coef, const u64* hcoef, const u64* zpts, u64* partial, u64* ood, int logn, int npoly,
-                int ext, hipStream_t s) {
+                int ext, hipStream_t s, const DeepCoinStep& dc) {
     const u64 n = 1ULL << logn;
     const int T = ood_threads(n), nblk = (int)(n / ((u64)T * OOD_R));
     if (ext == 2)
         hipLaunchKernelGGL(ood_kernel<2>, dim3(nblk, npoly), dim3(T), 0, s, coef, hcoef, zpts, partial, logn);
     else
         hipLaunchKernelGGL(ood_kernel<1>, dim3(nblk, npoly), dim3(T), 0, s, coef, hcoef, zpts, partial, logn);
-    hipLaunchKernelGGL(ood_final_kernel, dim3(npoly), dim3(64), 0, s, partial, nblk, ext, ood);
+    hipLaunchKernelGGL(ood_final_kernel, dim3(npoly), dim3(dc.coins ? 128 : 64), 0, s, partial, nblk, ext, ood, dc);
     XFG_CHECK_LAUNCH();
 }
 u64 ood_partial_count(int logn) {
@@ -730,206 +905,6 @@ void launch_fri_fold(const u64* vals, u64 val_stride, u64 comp_stride, bool cose
     dim3 g((unsigned)((rows + threads - 1) / threads), npoly);
     if (ext == 2) hipLaunchKernelGGL(fri_fold_kernel<2>, g, dim3(threads), 0, s, a);
     else hipLaunchKernelGGL(fri_fold_kernel<1>, g, dim3(threads), 0, s, a);
-    XFG_CHECK_LAUNCH();
-}
-
-// ============================================================================ device transcript
-__device__ __forceinline__ Digest dev_merge_int(const Digest& seed, u64 v) {
-    uint32_t m[16];
-#pragma unroll
-    for (int i = 0; i < 8; i++) m[i] = seed.w[i];
-    m[8] = (uint32_t)v;
-    m[9] = (uint32_t)(v >> 32);
-#pragma unroll
-    for (int i = 10; i < 16; i++) m[i] = 0;
-    return b3_hash_block(m, 40);
-}
-// Coin::draw_e: the first 8 D digest bytes as D LE elements, retried while any is >= p
-__device__ __forceinline__ bool dev_draw_e(DevCoin& c, u64* out, int D) {
-    for (int i = 0; i < 1000; i++) {
-        const Digest v = dev_merge_int(c.seed, ++c.counter);
-        const u64 x = (u64)v.w[0] | ((u64)v.w[1] << 32), y = (u64)v.w[2] | ((u64)v.w[3] << 32);
-        if (x < P && (D == 1 || y < P)) {
-            out[0] = x;
-            out[1] = D == 2 ? y : 0;
-            return true;
-        }
-    }
-    return false;
-}
-__device__ __forceinline__ void dev_reseed(DevCoin& c, const Digest& d) {
-    c.seed = b3_merge(c.seed, d);
-    c.counter = 0;
-}
-// Blake3_256::hash_elements of cnt <= 128 elements: one chunk of ceil(8 cnt / 64) blocks
-__device__ Digest dev_hash_elems(const u64* e, int cnt) {
-    uint32_t cv[8] = {XFG_B3_IV0, XFG_B3_IV1, XFG_B3_IV2, XFG_B3_IV3, XFG_B3_IV4, XFG_B3_IV5, XFG_B3_IV6, XFG_B3_IV7};
-    const int len = 8 * cnt, nb = (len + 63) / 64;
-    Digest d;
-    for (int blk = 0; blk < nb; blk++) {
-        uint32_t m[16];
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const int k = 8 * blk + i;
-            const u64 v = k < cnt ? e[k] : 0;
-            m[2 * i] = (uint32_t)v;
-            m[2 * i + 1] = (uint32_t)(v >> 32);
-        }
-        const bool last = blk == nb - 1;
-        const uint32_t flags = (blk == 0 ? B3_CHUNK_START : 0u) | (last ? B3_CHUNK_END | B3_ROOT : 0u);
-        uint32_t out[8];
-        b3_compress(cv, m, last ? (uint32_t)(len - 64 * blk) : 64u, 0, flags, out);
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            cv[i] = out[i];
-            d.w[i] = out[i];
-        }
-    }
-    return d;
-}
-// k <= 64 consecutive draws of E by one full wave, every lane holding the same coin: lane i hashes
-// counter + 1 + i at once, and the accepted candidates in counter order are exactly the draws
-// Coin::draw_e makes one after another (a rejected candidate is the one its retry skips). Draw j
-// goes to out[j S .. j S + D) (S = stride >= D). If the window holds fewer than k accepted candidates (>= 50
-// rejections of probability 2^-32 each) the rest are drawn one at a time after the last accepted.
-// The latency is one compression instead of k: these draws sit between two launches of the chain.
-__device__ bool wave_draw_e(DevCoin& c, int k, int D, u64* out, int S) {
-    const int lane = threadIdx.x & 63;
-    const Digest v = dev_merge_int(c.seed, c.counter + 1 + lane);
-    const u64 x = (u64)v.w[0] | ((u64)v.w[1] << 32), y = (u64)v.w[2] | ((u64)v.w[3] << 32);
-    const bool ok = x < P && (D == 1 || y < P);
-    const u64 mask = __ballot(ok);
-    const int idx = __popcll(mask & ((1ULL << lane) - 1));
-    if (ok && idx < k) {
-        out[idx * S] = x;
-        if (D == 2) out[idx * S + 1] = y;
-    }
-    const int got = __popcll(mask);
-    if (got >= k) {
-        u64 m = mask;
-        for (int i = 1; i < k; i++) m &= m - 1;  // lowest set bit = the k-th accepted candidate
-        c.counter += __ffsll((unsigned long long)m);
-        return true;
-    }
-    if (got > 0) c.counter += 64 - __clzll(mask);  // just past the last accepted candidate
-    bool all = true;
-    for (int j = got; j < k; j++) {
-        u64 a[2] = {0, 0};
-        all &= dev_draw_e(c, a, D);
-        if (lane == 0)
-            for (int d = 0; d < D; d++) out[j * S + d] = a[d];
-    }
-    return all;
-}
-// winter-prover Prover::prove after the trace commitment: reseed(trace root), draw the 15 constraint
-// composition coefficients (7 transition, 8 boundary); one wave per proof
-__global__ __launch_bounds__(64) void coin_coeffs_kernel(DevCoin* coins, const Digest* nodes, u64 node_stride,
-                                                         u64* coeffs, int* fail, int D) {
-    const int b = blockIdx.x;
-    DevCoin c = coins[b];
-    dev_reseed(c, nodes[(u64)b * node_stride + 1]);
-    const bool ok = wave_draw_e(c, 15, D, coeffs + (u64)b * 15 * D, D);
-    if (threadIdx.x == 0) {
-        if (!ok) fail[b] = 1;
-        coins[b] = c;
-    }
-}
-__global__ void coin_ood_point_kernel(DevCoin* coins, const Digest* nodes, u64 node_stride, u64 g, u64* zpts,
-                                      int* fail, int npoly, int D) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= npoly) return;
-    DevCoin c = coins[b];
-    dev_reseed(c, nodes[(u64)b * node_stride + 1]);
-    u64 z[2] = {0, 0};
-    bool ok = dev_draw_e(c, z, D);
-    if (z[0] == 0 && z[1] == 0) ok = false;  // z = 0 (then z g = 0 too): no DEEP quotient
-    for (int k = 0; k < D; k++) {
-        zpts[(u64)b * 2 * D + k] = z[k];
-        zpts[(u64)b * 2 * D + D + k] = gl_mul(z[k], g);
-    }
-    if (!ok) fail[b] = 1;
-    coins[b] = c;
-}
-// DEEP coefficients, two waves per proof: wave 0 runs the transcript (two element hashes, the 8
-// draws), wave 1 meanwhile inverts z (1 / (z g) = (1 / z) g^-1: one inversion)
-__global__ __launch_bounds__(128) void coin_deep_kernel(DevCoin* coins, const u64* ood, const u64* zpts, u64 ginv,
-                                                        DeepParams* dp, int* fail, int D) {
-    __shared__ u64 ab[8][2];  // a_0..a_6, gamma
-    __shared__ E2 zinv;
-    __shared__ int ok_s;
-    const int b = blockIdx.x;
-    const u64* o = ood + (u64)b * 15 * D;  // [T_c(z), T_c(zg)] x 7, H(z): E elements, coordinates interleaved
-    const u64* zb = zpts + (u64)b * 2 * D;
-    const E2 z{zb[0], D == 2 ? zb[1] : 0}, zg{zb[D], D == 2 ? zb[D + 1] : 0};
-    const bool zz = z.a == 0 && z.b == 0;  // z g == 0 <=> z == 0
-    if (threadIdx.x < 64) {
-        DevCoin c = coins[b];
-        dev_reseed(c, dev_hash_elems(o, 14 * D));
-        dev_reseed(c, dev_hash_elems(o + 14 * D, D));
-        const bool ok = wave_draw_e(c, 8, D, &ab[0][0], 2);
-        if (threadIdx.x == 0) {
-            coins[b] = c;
-            ok_s = ok;
-        }
-    } else if (threadIdx.x == 64) {
-        zinv = zz ? E2{0, 0} : e2_inv(z);
-    }
-    __syncthreads();
-    if (threadIdx.x != 0) return;
-    DeepParams P = {};
-    for (int k = 0; k < 7; k++)
-        for (int d = 0; d < D; d++) P.a[k][d] = ab[k][d];
-    for (int d = 0; d < D; d++) P.gamma[d] = ab[7][d];
-    auto put = [](u64* d, E2 v) { d[0] = v.a; d[1] = v.b; };
-    auto ood_e = [&](int q) { return E2{o[q * D], D == 2 ? o[q * D + 1] : 0}; };
-    put(P.z, z);
-    put(P.zg, zg);
-    put(P.zinv, zinv);
-    put(P.zginv, e2_mulb(zinv, ginv));
-    E2 c1 = e2_mul(E2{P.gamma[0], P.gamma[1]}, ood_e(14)), c2{0, 0};
-    for (int k = 0; k < 7; k++) {
-        const E2 a{P.a[k][0], P.a[k][1]};
-        c1 = e2_add(c1, e2_mul(a, ood_e(2 * k)));
-        c2 = e2_add(c2, e2_mul(a, ood_e(2 * k + 1)));
-    }
-    put(P.c1, c1);
-    put(P.c2, c2);
-    dp[b] = P;
-    if (!ok_s || zz) fail[b] = 1;
-}
-void launch_coin_coeffs(DevCoin* coins, const Digest* nodes, u64 node_stride, u64* coeffs, int* fail, int npoly,
-                        int ext, hipStream_t s) {
-    hipLaunchKernelGGL(coin_coeffs_kernel, dim3(npoly), dim3(64), 0, s, coins, nodes, node_stride, coeffs, fail, ext);
-    XFG_CHECK_LAUNCH();
-}
-void launch_coin_ood_point(DevCoin* coins, const Digest* nodes, u64 node_stride, u64 g, u64* zpts, int* fail,
-                           int npoly, int ext, hipStream_t s) {
-    hipLaunchKernelGGL(coin_ood_point_kernel, dim3((npoly + 63) / 64), dim3(64), 0, s, coins, nodes, node_stride, g,
-                       zpts, fail, npoly, ext);
-    XFG_CHECK_LAUNCH();
-}
-void launch_coin_deep(DevCoin* coins, const u64* ood, const u64* zpts, u64 ginv, DeepParams* dp, int* fail, int npoly,
-                      int ext, hipStream_t s) {
-    hipLaunchKernelGGL(coin_deep_kernel, dim3(npoly), dim3(128), 0, s, coins, ood, zpts, ginv, dp, fail, ext);
-    XFG_CHECK_LAUNCH();
-}
-__global__ void fri_alpha_kernel(DevCoin* coins, const Digest* nodes, u64 node_stride, u64* alpha7, int* fail,
-                                 int npoly, int D) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= npoly) return;
-    DevCoin c = coins[b];
-    c.seed = b3_merge(c.seed, nodes[(u64)b * node_stride + 1]);  // reseed: counter restarts
-    c.counter = 0;
-    u64 a[2] = {0, 0};
-    if (!dev_draw_e(c, a, D)) fail[b] = 1;
-    const u64 inv7 = 0x249249246DB6DB6EULL;  // 7^-1 mod p
-    for (int k = 0; k < D; k++) alpha7[(u64)b * D + k] = gl_mul(a[k], inv7);
-    coins[b] = c;
-}
-void launch_fri_alpha(DevCoin* coins, const Digest* nodes, u64 node_stride, u64* alpha7, int* fail, int npoly,
-                      int ext, hipStream_t s) {
-    hipLaunchKernelGGL(fri_alpha_kernel, dim3((npoly + 63) / 64), dim3(64), 0, s, coins, nodes, node_stride, alpha7,
-                       fail, npoly, ext);
     XFG_CHECK_LAUNCH();
 }
 

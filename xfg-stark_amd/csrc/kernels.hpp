@@ -56,6 +56,38 @@ void launch_field_op(int op, const u64* a, const u64* b, u64* out, u64 count, hi
 void launch_interpolate(const u64* evals, u64 in_stride, u64* out, u64 out_stride, u64* scratch, int npoly, int logn,
                         bool off7, u64 keep, const Tables& T, hipStream_t s);
 
+// ---- device-side Fiat-Shamir (winter-crypto DefaultRandomCoin<Blake3_256>, as host_common.hpp Coin).
+// Each transcript step runs in the kernel that produces its input, one proof per block; the host
+// replays the same steps from the roots and the OOD frame afterwards. fail[b] = 1 when a draw was
+// rejected 1000 times in a row or z = 0.
+struct DevCoin {
+    Digest seed;
+    u64 counter;
+    u64 pad;
+};
+// step run on a Merkle root by launch_tree_top: reseed with the root, then
+//   COEFFS (trace root): the 15 composition coefficients -> out = coeffs [B][15][D]
+//   OOD_POINT (composition root): z -> out = zpts [B][2][D] = (z, z g)
+//   FRI_ALPHA (FRI layer root): alpha -> out = alpha7 [B][D] = alpha * 7^-1
+struct CoinStep {
+    enum Kind : int { NONE = 0, COEFFS = 1, OOD_POINT = 2, FRI_ALPHA = 3 };
+    int kind = NONE;
+    int ext = 1;
+    DevCoin* coins = nullptr;
+    int* fail = nullptr;
+    u64* out = nullptr;
+    u64 g = 0;  // OOD_POINT: the trace domain generator
+};
+// step run by launch_ood on the OOD frame (when coins is set): reseed with hash(trace frame) and
+// hash(H(z)), draw a_0..a_6 and gamma, and form the DEEP parameters dp [B] from zpts [B][2][D]
+struct DeepCoinStep {
+    DevCoin* coins = nullptr;
+    int* fail = nullptr;
+    const u64* zpts = nullptr;
+    DeepParams* dp = nullptr;
+    u64 ginv = 0;  // g^-1
+};
+
 // ---- Merkle (heap layout: nodes[1] = root, nodes[L + i] = leaf i) ----
 // LDE commitments store levels >= log2(beta) + 1 only: node_stride >= 2n; the subtree over rows
 // (2j, 2j+1) tops out at heap node n/2 + j; launch_tree_top(nodes, stride, n / 2, ...) finishes
@@ -72,8 +104,10 @@ void launch_open_rows(const u64* lde, int nc, const u64* entries, u64 count, Dig
 // (returns the node count left for launch_tree_top, like launch_leaves_lde)
 u64 launch_fri_leaves(const u64* vals, u64 val_stride, u64 comp_stride, bool coset_major, int logn, int logbeta,
                       u64 rows, Digest* nodes, u64 node_stride, int npoly, int ext, hipStream_t s);
-// completes the tree above level `count` (nodes [count, 2count) present) up to the root
-void launch_tree_top(Digest* nodes, u64 node_stride, u64 count, int npoly, hipStream_t s);
+// completes the tree above level `count` (nodes [count, 2count) present) up to the root, then runs
+// the transcript step `cs` on it
+void launch_tree_top(Digest* nodes, u64 node_stride, u64 count, int npoly, hipStream_t s,
+                     const CoinStep& cs = CoinStep{});
 
 // ---- AIR ----
 void launch_trace_gen(const AirConst* air, u64* trace, int logn, int npoly, hipStream_t s);
@@ -87,7 +121,7 @@ void launch_constraint_eval(const u64* lde, const AirConst* air, const u64* coef
 // partial: [B][ood_partial_count(logn)][15] per-block sums, kept for launch_deep
 // ext = D: zpts [B][2][D], hcoef planes [B][D][n], partial [B][count][15][D], ood [B][15][D]
 void launch_ood(const u64* coef, const u64* hcoef, const u64* zpts, u64* partial, u64* ood, int logn, int npoly,
-                int ext, hipStream_t s);
+                int ext, hipStream_t s, const DeepCoinStep& dc = DeepCoinStep{});
 u64 ood_partial_count(int logn);
 // carry: [B][ood_partial_count(logn)][2][D]; deep planes [B][D][n]
 void launch_deep(const u64* coef, const u64* hcoef, const DeepParams* dp, const u64* partial, u64* carry, u64* deep,
@@ -98,30 +132,6 @@ void launch_deep(const u64* coef, const u64* hcoef, const DeepParams* dp, const 
 void launch_fri_fold(const u64* vals, u64 val_stride, u64 comp_stride, bool coset_major, int logn, int logbeta,
                      u64 rows, int logD, const u64* alpha7, u64* out, u64 out_stride, const Tables& T, int npoly,
                      int ext, hipStream_t s);
-
-// ---- device-side Fiat-Shamir (winter-crypto DefaultRandomCoin<Blake3_256>, as host_common.hpp Coin)
-struct DevCoin {
-    Digest seed;
-    u64 counter;
-    u64 pad;
-};
-// FRI layer step of the transcript on the device, one thread per proof: reseed with the layer's
-// Merkle root (heap node 1 of the proof's tree, nodes + b * node_stride), draw alpha in E (retried
-// while >= p, at most 1000 times) and write alpha7 [B][D] = alpha * 7^-1; fail[b] = 1 when every
-// draw was rejected. The host replays the same steps from the roots afterwards.
-void launch_fri_alpha(DevCoin* coins, const Digest* nodes, u64 node_stride, u64* alpha7, int* fail, int npoly,
-                      int ext, hipStream_t s);
-// the earlier transcript steps, same conventions (fail[b] = 1 on a rejected draw or a zero OOD point):
-// reseed with the trace root, draw the 15 composition coefficients -> coeffs [B][15][D]
-void launch_coin_coeffs(DevCoin* coins, const Digest* nodes, u64 node_stride, u64* coeffs, int* fail, int npoly,
-                        int ext, hipStream_t s);
-// reseed with the composition root, draw z -> zpts [B][2][D] = (z, z g)
-void launch_coin_ood_point(DevCoin* coins, const Digest* nodes, u64 node_stride, u64 g, u64* zpts, int* fail,
-                           int npoly, int ext, hipStream_t s);
-// reseed with hash(trace OOD frame), hash(H(z)) (ood [B][15][D]), draw a_0..a_6, gamma -> dp [B]
-// (ginv = g^-1, the trace domain generator's inverse)
-void launch_coin_deep(DevCoin* coins, const u64* ood, const u64* zpts, u64 ginv, DeepParams* dp, int* fail, int npoly,
-                      int ext, hipStream_t s);
 
 // ---- openings ----
 void launch_gather_u64(const u64* src, const u64* idx, u64* dst, u64 count, hipStream_t s);

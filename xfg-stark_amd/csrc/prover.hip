@@ -591,12 +591,16 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     launch_lde(c->coef.p, n, c->lde.p, c->scratch.p, B * 7, logn, logbeta, T, s);
     if (probe) HIPCHK(hipEventRecord(c->lde_ev[1], s));
     stage_mark(c, 1);
+    // ---- 2. trace root -> constraint composition coefficients (7 transition + 8 boundary)
+    CoinStep cs;
+    cs.ext = DE;
+    cs.coins = c->dcoin.p;
+    cs.fail = c->dfail.p;
+    cs.kind = CoinStep::COEFFS;
+    cs.out = c->coeffs.p;
     launch_tree_top(c->tnodes.p, 2 * n, launch_leaves_lde(c->lde.p, 7, c->tnodes.p, 2 * n, B, logn, logbeta, s), B,
-                    s);
+                    s, cs);
     stage_mark(c, 2);
-
-    // ---- 2. constraint composition coefficients (7 transition + 8 boundary)
-    launch_coin_coeffs(c->dcoin.p, c->tnodes.p, 2 * n, c->coeffs.p, c->dfail.p, B, DE, s);
 
     // ---- 3. constraint evaluation + composition polynomial + commitment
     launch_constraint_eval(c->lde.p, c->air.p, c->coeffs.p, ce_div, c->ce.p, logn, logbeta, B, DE, s);
@@ -604,17 +608,23 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     launch_interpolate(c->ce.p, 2 * n, c->hcoef.p, n, c->scratch.p, B * DE, logn + 1, true, n, T, s);
     launch_lde(c->hcoef.p, n, c->hlde.p, c->scratch.p, B * DE, logn, logbeta, T, s);
     stage_mark(c, 4);
+    // ---- 4. composition root -> OOD point (z, z g); the frame, then the DEEP draws
+    cs.kind = CoinStep::OOD_POINT;
+    cs.out = c->zpts.p;
+    cs.g = gl_root(logn);
     launch_tree_top(c->hnodes.p, 2 * n, launch_leaves_lde(c->hlde.p, DE, c->hnodes.p, 2 * n, B, logn, logbeta, s), B,
-                    s);
+                    s, cs);
     stage_mark(c, 5);
-
-    // ---- 4. OOD point (z, z g) and frame
-    launch_coin_ood_point(c->dcoin.p, c->hnodes.p, 2 * n, gl_root(logn), c->zpts.p, c->dfail.p, B, DE, s);
-    launch_ood(c->coef.p, c->hcoef.p, c->zpts.p, c->partial.p, c->ood.p, logn, B, DE, s);
+    DeepCoinStep dc;
+    dc.coins = c->dcoin.p;
+    dc.fail = c->dfail.p;
+    dc.zpts = c->zpts.p;
+    dc.dp = c->dp.p;
+    dc.ginv = gl_inv(cs.g);
+    launch_ood(c->coef.p, c->hcoef.p, c->zpts.p, c->partial.p, c->ood.p, logn, B, DE, s, dc);
     stage_mark(c, 6);
 
     // ---- 5. DEEP composition polynomial (coefficient form) + its LDE
-    launch_coin_deep(c->dcoin.p, c->ood.p, c->zpts.p, gl_inv(gl_root(logn)), c->dp.p, c->dfail.p, B, DE, s);
     launch_deep(c->coef.p, c->hcoef.p, c->dp.p, c->partial.p, c->carry.p, c->deep.p, logn, B, DE, s);
     launch_lde(c->deep.p, n, c->f0.p, c->scratch.p, B * DE, logn, logbeta, T, s);
     // degree check: deg(DEEP) == n - 2  <=>  coefficient n-2 != 0 (coefficient n-1 is 0 by construction)
@@ -630,8 +640,9 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         const u64 cstride = cm ? N : D[l], sstride = DE * cstride;
         u64 top = launch_fri_leaves(src, sstride, cstride, cm, logn, logbeta, rows, c->fnodes[l].p, 2 * rows, B, DE,
                                     s);
-        launch_tree_top(c->fnodes[l].p, 2 * rows, top, B, s);
-        launch_fri_alpha(c->dcoin.p, c->fnodes[l].p, 2 * rows, c->alpha7.p, c->dfail.p, B, DE, s);
+        cs.kind = CoinStep::FRI_ALPHA;
+        cs.out = c->alpha7.p;
+        launch_tree_top(c->fnodes[l].p, 2 * rows, top, B, s, cs);
         launch_fri_fold(src, sstride, cstride, cm, logn, logbeta, rows, (int)ilog2(D[l]), c->alpha7.p,
                         c->flayer[l + 1].p, rows, T, B, DE, s);
     }
