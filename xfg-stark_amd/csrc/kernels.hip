@@ -917,6 +917,27 @@ __global__ void gather_digest_kernel(const Digest* src, const u64* idx, Digest* 
     u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < count) dst[i] = src[idx[i]];
 }
+// all of a unit's opening gathers in one launch: thread i of the grid serves element i - first[k] of
+// segment k (the segments are laid end to end in index order; at most GatherSet::MAX of them)
+__global__ void gather_set_kernel(GatherSet g, const u64* idx) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= g.first[g.nseg]) return;
+    int k = 0;
+    while (i >= g.first[k + 1]) k++;
+    const u64 src = idx[i];
+    if (g.digest[k]) {
+        const Digest* s = (const Digest*)g.src[k];
+        ((Digest*)g.dst[k])[i - g.first[k]] = s[src];
+    } else {
+        ((u64*)g.dst[k])[i - g.first[k]] = ((const u64*)g.src[k])[src];
+    }
+}
+void launch_gather_set(const GatherSet& g, const u64* idx, hipStream_t s) {
+    const u64 total = g.first[g.nseg];
+    if (!total) return;
+    hipLaunchKernelGGL(gather_set_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, g, idx);
+    XFG_CHECK_LAUNCH();
+}
 void launch_gather_u64(const u64* src, const u64* idx, u64* dst, u64 count, hipStream_t s) {
     if (!count) return;
     hipLaunchKernelGGL(gather_u64_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s, src, idx, dst, count);

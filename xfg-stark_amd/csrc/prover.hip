@@ -855,19 +855,29 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     HIPCHK(hipMemcpyAsync(c->gidx.p, hidx, allidx.size() * 8, hipMemcpyHostToDevice, s));
     ht.mark("q_h2d");
     {
-        size_t vo = 0;
+        // the segments lie end to end in allidx: values first, then digests
+        GatherSet gs;
+        size_t vo = 0, dof = 0;
+        auto add = [&](const void* src, void* dst, bool dig, size_t cnt) {
+            if (gs.nseg == GatherSet::MAX) throw std::runtime_error("too many FRI layers for one gather launch");
+            gs.src[gs.nseg] = src;
+            gs.dst[gs.nseg] = dst;
+            gs.digest[gs.nseg] = dig ? 1 : 0;
+            gs.first[gs.nseg + 1] = gs.first[gs.nseg] + cnt;
+            gs.nseg++;
+        };
         const u64* vsrc[2] = {c->lde.p, c->hlde.p};
         for (size_t k = 0; k < vseg.size(); k++) {
             const u64* src = k < 2 ? vsrc[k] : (k == 2 ? c->f0.p : c->flayer[k - 2].p);
-            launch_gather_u64(src, c->gidx.p + vseg[k].first, c->gval.p + vo, vseg[k].second, s);
+            add(src, c->gval.p + vo, false, vseg[k].second);
             vo += vseg[k].second;
         }
-        size_t dof = 0;
         for (size_t k = 0; k < dseg.size(); k++) {
             const Digest* src = k == 0 ? c->tnodes.p : (k == 1 ? c->hnodes.p : c->fnodes[k - 2].p);
-            launch_gather_digest(src, c->gidx.p + dseg[k].first, c->gdig.p + dof, dseg[k].second, s);
+            add(src, c->gdig.p + dof, true, dseg[k].second);
             dof += dseg[k].second;
         }
+        launch_gather_set(gs, c->gidx.p, s);
         const u64* ent = c->gidx.p + nvals + ndig;
         launch_open_rows(c->lde.p, 7, ent, nent, c->gdig.p + ndig, logn, logbeta, s);
         launch_open_rows(c->hlde.p, DE, ent, nent, c->gdig.p + ndig + nopen, logn, logbeta, s);
