@@ -148,6 +148,7 @@ __device__ void coin_root_step(const CoinStep& cs, int b, const Digest& root) {
     if (lane == 0) {
         if (!ok) cs.fail[b] = 1;
         cs.coins[b] = c;
+        if (cs.root_out) cs.root_out[b] = root;
     }
 }
 

@@ -274,9 +274,9 @@ struct Lane {
     DBuf<AirConst> air;
     DBuf<u64> coeffs, trace, coef, scratch, lde, ce, hcoef, hlde, zpts, partial, ood, carry, deep, f0, alpha7,
         rem, gidx, gval, dn2;
-    DBuf<Digest> tnodes, hnodes, gdig;
+    DBuf<Digest> tnodes, hnodes, gdig, droots;
     DBuf<DeepParams> dp;
-    DBuf<DevCoin> dcoin;  // device-side transcript (FRI rounds)
+    DBuf<DevCoin> dcoin;  // device-side transcript
     DBuf<int> dfail;
     std::vector<DBuf<u64>> flayer;
     std::vector<DBuf<Digest>> fnodes;
@@ -286,7 +286,6 @@ struct Lane {
     HBuf<AirConst> h_air;
     HBuf<DevCoin> h_coin;
     HBuf<DeepParams> h_dp;
-    HBuf<Digest> h_froots;
     HBuf<int> h_fail;
     // host scratch of the opening plans and the serialiser, kept across units so steady-state
     // units neither allocate nor page-fault (their cost grew with the shared hosts' load)
@@ -301,7 +300,6 @@ struct Lane {
         h_air.release();
         h_coin.release();
         h_dp.release();
-        h_froots.release();
         h_fail.release();
         dcoin.release();
         dfail.release();
@@ -309,7 +307,7 @@ struct Lane {
         for (auto* b : {&coeffs, &trace, &coef, &scratch, &lde, &ce, &hcoef, &hlde, &zpts, &partial, &ood,
                         &carry, &deep, &f0, &alpha7, &rem, &gidx, &gval, &dn2})
             b->release();
-        for (auto* b : {&tnodes, &hnodes, &gdig}) b->release();
+        for (auto* b : {&tnodes, &hnodes, &gdig, &droots}) b->release();
         dp.release();
         for (auto& b : flayer) b.release();
         for (auto& b : fnodes) b.release();
@@ -596,8 +594,10 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     cs.ext = DE;
     cs.coins = c->dcoin.p;
     cs.fail = c->dfail.p;
+    c->droots.ensure((size_t)(2 + nl) * B);  // trace, composition, FRI layer roots: [tree][B]
     cs.kind = CoinStep::COEFFS;
     cs.out = c->coeffs.p;
+    cs.root_out = c->droots.p;
     launch_tree_top(c->tnodes.p, 2 * n, launch_leaves_lde(c->lde.p, 7, c->tnodes.p, 2 * n, B, logn, logbeta, s), B,
                     s, cs);
     stage_mark(c, 2);
@@ -611,6 +611,7 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     // ---- 4. composition root -> OOD point (z, z g); the frame, then the DEEP draws
     cs.kind = CoinStep::OOD_POINT;
     cs.out = c->zpts.p;
+    cs.root_out = c->droots.p + B;
     cs.g = gl_root(logn);
     launch_tree_top(c->hnodes.p, 2 * n, launch_leaves_lde(c->hlde.p, DE, c->hnodes.p, 2 * n, B, logn, logbeta, s), B,
                     s, cs);
@@ -642,28 +643,23 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
                                     s);
         cs.kind = CoinStep::FRI_ALPHA;
         cs.out = c->alpha7.p;
+        cs.root_out = c->droots.p + (size_t)(2 + l) * B;
         launch_tree_top(c->fnodes[l].p, 2 * rows, top, B, s, cs);
         launch_fri_fold(src, sstride, cstride, cm, logn, logbeta, rows, (int)ilog2(D[l]), c->alpha7.p,
                         c->flayer[l + 1].p, rows, T, B, DE, s);
     }
     ht.mark("chain_launch");
     // transcript inputs for the host replay: trace / composition roots, OOD frame, FRI roots
-    Digest* roots = c->h_roots.ensure((size_t)2 * B);
-    HIPCHK(hipMemcpy2DAsync(roots, sizeof(Digest), c->tnodes.p + 1, 2 * n * sizeof(Digest), sizeof(Digest), B,
-                            hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpy2DAsync(roots + B, sizeof(Digest), c->hnodes.p + 1, 2 * n * sizeof(Digest), sizeof(Digest), B,
-                            hipMemcpyDeviceToHost, s));
+    Digest* roots = c->h_roots.ensure((size_t)(2 + nl) * B);  // [trace, composition, FRI 0..nl-1][B]
+    HIPCHK(hipMemcpyAsync(roots, c->droots.p, (size_t)(2 + nl) * B * sizeof(Digest), hipMemcpyDeviceToHost, s));
     u64* ood = c->h_ood.ensure((size_t)B * 15 * DE);
     HIPCHK(hipMemcpyAsync(ood, c->ood.p, (size_t)B * 15 * DE * 8, hipMemcpyDeviceToHost, s));
     u64* co = c->h_co.ensure((size_t)B * 15 * DE);  // the device's draws, checked by the replay
     HIPCHK(hipMemcpyAsync(co, c->coeffs.p, (size_t)B * 15 * DE * 8, hipMemcpyDeviceToHost, s));
     DeepParams* dps = c->h_dp.ensure(B);
     HIPCHK(hipMemcpyAsync(dps, c->dp.p, B * sizeof(DeepParams), hipMemcpyDeviceToHost, s));
-    Digest* froots = c->h_froots.ensure((size_t)std::max(1u, nl) * B);
+    const Digest* froots = roots + 2 * B;
     int* ffail = c->h_fail.ensure(B);
-    for (unsigned l = 0; l < nl; l++)
-        HIPCHK(hipMemcpy2DAsync(froots + (size_t)l * B, sizeof(Digest), c->fnodes[l].p + 1,
-                                2 * (D[l] / 8) * sizeof(Digest), sizeof(Digest), B, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(ffail, c->dfail.p, B * sizeof(int), hipMemcpyDeviceToHost, s));
     // remainder: interpolate the last layer over 7*<w_D>, keep D/blowup coefficients
     // (with no folding layer this is the DEEP polynomial's own coefficients)
