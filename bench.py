@@ -239,7 +239,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-config5", action="store_true", help="skip the configs[4] side measurement")
-    ap.add_argument("--depth", type=int, default=3, help="batches in flight (pipelined submission)")
+    ap.add_argument("--depth", type=int, default=6, help="batches in flight (pipelined submission)")
     args = ap.parse_args()
 
     import torch
