@@ -1041,12 +1041,12 @@ static int max_lanes() {
     static const int v = std::max(1, env_int("XFG_LANES", 7));
     return v;
 }
-// 22 proofs per unit: a 64-proof batch becomes 22 + 22 + 20. Same box, 3 x 40 steps, with the unit's
-// transcript on the device: 11,400 +- 58 burn-proofs/s against 11,075 +- 103 with 20 (20 + 20 + 20 + 4),
-// 11,407 with 24, 11,302 with 23, 11,254-11,269 with 26-28, 10,790 with 32, 10,925 with 16.
-// (With host round trips between the stages 20 had been best: 10,680 against 10,592 with 24.)
+// 32 proofs per unit: a 64-proof batch is two units. Same box, 3 x 20 steps at bench.py's depth 6:
+// 12,069 +- 70 burn-proofs/s against 11,890 +- 50 with 22, 11,645 with 64, 11,557 with 16. (At depth
+// 3 the unit queue ran dry and smaller units won: 22 gave 11,400 against 10,790 with 32; with the
+// transcript's host round trips still in place 20 had been best.)
 static int unit_size() {
-    static const int v = std::max(1, env_int("XFG_UNIT", 22));
+    static const int v = std::max(1, env_int("XFG_UNIT", 32));
     return v;
 }
 
