@@ -140,9 +140,10 @@ def pipelined_steps(submit_fn, collect_fn, batches, rank, world, per_rank, devic
     return out
 
 
-def config5(prover, batch=4, calls=5):
+def config5(prover, batch=4, calls=8, depth=4):
     """side measurement of BASELINE configs[4]: 2^20-step trace, blowup 16, 96-bit class options
-    (quadratic extension, 24 queries, grinding 4), batches of `batch` proofs per call on this GPU"""
+    (quadratic extension, 24 queries, grinding 4), batches of `batch` proofs per call on this GPU,
+    `depth` calls in flight"""
     import xfgstark
     n5 = 1 << 20
     o = xfgstark.ProofOptions.reference()
@@ -152,14 +153,14 @@ def config5(prover, batch=4, calls=5):
     try:
         prover.prepare(batch, n5)
         kws = [synthetic.burn_inputs(50_000 + i) for i in range(batch)]
-        pend = None
+        pend = []
         t = time.perf_counter()
         for _ in range(calls):
-            nxt = prover.submit_batch(kws, trace_length=n5)
-            if pend is not None:
-                pend.result()
-            pend = nxt
-        res = pend.result()
+            pend.append(prover.submit_batch(kws, trace_length=n5))
+            if len(pend) >= depth:
+                pend.pop(0).result()
+        while pend:
+            res = pend.pop(0).result()
         dt = time.perf_counter() - t
         assert all(not isinstance(r, Exception) for r in res)
         lde_ms = prover.bench_lde(1, n5, 16, 5)
