@@ -189,6 +189,15 @@ int xfg_debug_field(xfg_ctx* ctx, uint32_t op, uint64_t count, const uint64_t* a
  * T_c(zg) interleaved, H(z)), deep_out [count][n] (DEEP composition coefficients) */
 int xfg_debug_ood_deep(xfg_ctx* ctx, uint32_t count, uint64_t n, const uint64_t* coef, const uint64_t* hcoef,
                        const uint64_t* zpts, const uint64_t* coeffs, uint64_t* ood_out, uint64_t* deep_out);
+/* device Fiat-Shamir draws (DefaultRandomCoin<Blake3_256>::draw::<E>) from the coin (seed as 8 LE
+ * u32 words, counter): k <= 64 draws of E (ext 1 or 2) by one wave -- the prover's coefficient and
+ * DEEP draws -- and one at a time -- its FRI alpha draws. Besides the >= p rule, a candidate whose
+ * counter c (1 <= c <= 256) has bit c - 1 of reject[4] set is rejected, to exercise the retries.
+ * out_wave / out_seq [k][2] (second coordinate 0 when ext = 1), counters[2] = each coin's counter
+ * afterwards, ok[2] = 1 when no draw ran out of its 1000 tries */
+int xfg_debug_coin_draws(xfg_ctx* ctx, const uint32_t seed[8], uint64_t counter, uint32_t k, uint32_t ext,
+                         const uint64_t reject[4], uint64_t* out_wave, uint64_t* out_seq, uint64_t counters[2],
+                         int ok[2]);
 
 #ifdef __cplusplus
 }

@@ -44,12 +44,17 @@ __device__ __forceinline__ Digest dev_merge_int(const Digest& seed, u64 v) {
     for (int i = 10; i < 16; i++) m[i] = 0;
     return b3_hash_block(m, 40);
 }
+// acceptance of a drawn candidate (counter, first two LE words): every element < p
+struct AcceptP {
+    __device__ bool operator()(u64, u64 x, u64 y, int D) const { return x < P && (D == 1 || y < P); }
+};
 // Coin::draw_e: the first 8 D digest bytes as D LE elements, retried while any is >= p
-__device__ __forceinline__ bool dev_draw_e(DevCoin& c, u64* out, int D) {
+template <class A = AcceptP>
+__device__ __forceinline__ bool dev_draw_e(DevCoin& c, u64* out, int D, A acc = A()) {
     for (int i = 0; i < 1000; i++) {
         const Digest v = dev_merge_int(c.seed, ++c.counter);
         const u64 x = (u64)v.w[0] | ((u64)v.w[1] << 32), y = (u64)v.w[2] | ((u64)v.w[3] << 32);
-        if (x < P && (D == 1 || y < P)) {
+        if (acc(c.counter, x, y, D)) {
             out[0] = x;
             out[1] = D == 2 ? y : 0;
             return true;
@@ -93,11 +98,12 @@ __device__ Digest dev_hash_elems(const u64* e, int cnt) {
 // goes to out[j S .. j S + D) (S = stride >= D). If the window holds fewer than k accepted candidates (>= 50
 // rejections of probability 2^-32 each) the rest are drawn one at a time after the last accepted.
 // The latency is one compression instead of k: these draws sit between two launches of the chain.
-__device__ bool wave_draw_e(DevCoin& c, int k, int D, u64* out, int S) {
+template <class A = AcceptP>
+__device__ bool wave_draw_e(DevCoin& c, int k, int D, u64* out, int S, A acc = A()) {
     const int lane = threadIdx.x & 63;
     const Digest v = dev_merge_int(c.seed, c.counter + 1 + lane);
     const u64 x = (u64)v.w[0] | ((u64)v.w[1] << 32), y = (u64)v.w[2] | ((u64)v.w[3] << 32);
-    const bool ok = x < P && (D == 1 || y < P);
+    const bool ok = acc(c.counter + 1 + lane, x, y, D);
     const u64 mask = __ballot(ok);
     const int idx = __popcll(mask & ((1ULL << lane) - 1));
     if (ok && idx < k) {
@@ -115,7 +121,7 @@ __device__ bool wave_draw_e(DevCoin& c, int k, int D, u64* out, int S) {
     bool all = true;
     for (int j = got; j < k; j++) {
         u64 a[2] = {0, 0};
-        all &= dev_draw_e(c, a, D);
+        all &= dev_draw_e(c, a, D, acc);
         if (lane == 0)
             for (int d = 0; d < D; d++) out[j * S + d] = a[d];
     }
@@ -906,6 +912,44 @@ void launch_fri_fold(const u64* vals, u64 val_stride, u64 comp_stride, bool cose
     dim3 g((unsigned)((rows + threads - 1) / threads), npoly);
     if (ext == 2) hipLaunchKernelGGL(fri_fold_kernel<2>, g, dim3(threads), 0, s, a);
     else hipLaunchKernelGGL(fri_fold_kernel<1>, g, dim3(threads), 0, s, a);
+    XFG_CHECK_LAUNCH();
+}
+
+// ============================================================================ transcript self test
+// AcceptP plus forced rejections: candidate counter c in [1, 256] is rejected when bit c - 1 of
+// rej[4] is set (exercises wave_draw_e's window bookkeeping and its one-at-a-time fallback)
+struct AcceptForced {
+    const u64* rej;
+    __device__ bool operator()(u64 ctr, u64 x, u64 y, int D) const {
+        const bool forced = ctr >= 1 && ctr <= 256 && ((rej[(ctr - 1) >> 6] >> ((ctr - 1) & 63)) & 1);
+        return !forced && AcceptP()(ctr, x, y, D);
+    }
+};
+__global__ __launch_bounds__(64) void coin_draw_test_kernel(DevCoin c0, int k, int D, const u64* rej, u64* out_wave,
+                                                            u64* out_seq, u64* ctr, int* ok) {
+    const AcceptForced acc{rej};
+    DevCoin c = c0;
+    const bool okw = wave_draw_e(c, k, D, out_wave, 2, acc);
+    DevCoin q = c0;
+    bool oks = true;
+    for (int j = 0; j < k; j++) {
+        u64 a[2] = {0, 0};
+        oks &= dev_draw_e(q, a, D, acc);
+        if (threadIdx.x == 0) {
+            out_seq[2 * j] = a[0];
+            out_seq[2 * j + 1] = a[1];
+        }
+    }
+    if (threadIdx.x == 0) {
+        ctr[0] = c.counter;
+        ctr[1] = q.counter;
+        ok[0] = okw;
+        ok[1] = oks;
+    }
+}
+void launch_coin_draw_test(const DevCoin& c0, int k, int ext, const u64* rej, u64* out_wave, u64* out_seq, u64* ctr,
+                           int* ok, hipStream_t s) {
+    hipLaunchKernelGGL(coin_draw_test_kernel, dim3(1), dim3(64), 0, s, c0, k, ext, rej, out_wave, out_seq, ctr, ok);
     XFG_CHECK_LAUNCH();
 }
 

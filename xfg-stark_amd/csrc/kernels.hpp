@@ -89,6 +89,11 @@ struct DeepCoinStep {
     u64 ginv = 0;  // g^-1
 };
 
+// self test of the draw paths (xfg_debug_coin_draws): from coin c0, k <= 64 draws by one wave
+// (out_wave) and one at a time (out_seq), both [k][2]; counters after each in ctr[2], success in ok[2]
+void launch_coin_draw_test(const DevCoin& c0, int k, int ext, const u64* rej, u64* out_wave, u64* out_seq, u64* ctr,
+                           int* ok, hipStream_t s);
+
 // ---- Merkle (heap layout: nodes[1] = root, nodes[L + i] = leaf i) ----
 // LDE commitments store levels >= log2(beta) + 1 only: node_stride >= 2n; the subtree over rows
 // (2j, 2j+1) tops out at heap node n/2 + j; launch_tree_top(nodes, stride, n / 2, ...) finishes

@@ -1646,6 +1646,41 @@ int xfg_debug_field(xfg_ctx* c, uint32_t op, uint64_t count, const uint64_t* a, 
     });
 }
 
+int xfg_debug_coin_draws(xfg_ctx* c, const uint32_t seed[8], uint64_t counter, uint32_t k, uint32_t ext,
+                         const uint64_t reject[4], uint64_t* out_wave, uint64_t* out_seq, uint64_t counters[2],
+                         int ok[2]) {
+    if (!c || !seed || !reject || !out_wave || !out_seq || !counters || !ok || k == 0 || k > 64 ||
+        (ext != 1 && ext != 2))
+        return XFG_INVALID_ARGUMENT;
+    if (busy(c)) {
+        c->err = "batches pending: call xfg_batch_wait first";
+        return XFG_INVALID_ARGUMENT;
+    }
+    return guarded(c, [&]() -> int {
+        Lane* L = lane0(c);
+        HIPCHK(hipSetDevice(c->device));
+        L->trace.ensure(4 + 4 * (size_t)k + 2 + 1);
+        u64* drej = L->trace.p;
+        u64* dw = drej + 4;
+        u64* ds = dw + 2 * k;
+        u64* dctr = ds + 2 * k;
+        int* dok = (int*)(dctr + 2);
+        HIPCHK(hipMemcpy(drej, reject, 32, hipMemcpyHostToDevice));
+        HIPCHK(hipMemset(dw, 0, 16 * (size_t)k));
+        DevCoin c0;
+        memcpy(c0.seed.w, seed, 32);
+        c0.counter = counter;
+        c0.pad = 0;
+        launch_coin_draw_test(c0, (int)k, (int)ext, drej, dw, ds, dctr, dok, L->stream);
+        HIPCHK(hipMemcpyAsync(out_wave, dw, 16 * (size_t)k, hipMemcpyDeviceToHost, L->stream));
+        HIPCHK(hipMemcpyAsync(out_seq, ds, 16 * (size_t)k, hipMemcpyDeviceToHost, L->stream));
+        HIPCHK(hipMemcpyAsync(counters, dctr, 16, hipMemcpyDeviceToHost, L->stream));
+        HIPCHK(hipMemcpyAsync(ok, dok, 8, hipMemcpyDeviceToHost, L->stream));
+        HIPCHK(hipStreamSynchronize(L->stream));
+        return XFG_OK;
+    });
+}
+
 int xfg_debug_ood_deep(xfg_ctx* c, uint32_t count, uint64_t n, const uint64_t* coef, const uint64_t* hcoef,
                        const uint64_t* zpts, const uint64_t* coeffs, uint64_t* ood_out, uint64_t* deep_out) {
     if (!c || !coef || !hcoef || !zpts || !coeffs || !ood_out || !deep_out || !is_pow2(n) || n < 8 || count == 0)

@@ -88,6 +88,9 @@ _lib.xfg_debug_ood_deep.argtypes = [C.c_void_p, C.c_uint32, C.c_uint64, _u64p, _
 _lib.xfg_debug_interpolate.argtypes = [C.c_void_p, _u64p, C.c_uint32, C.c_uint64, C.c_int, _u64p]
 if hasattr(_lib, "xfg_debug_field"):  # absent from builds older than the primitive self test (XFG_LIB A/B)
     _lib.xfg_debug_field.argtypes = [C.c_void_p, C.c_uint32, C.c_uint64, _u64p, _u64p, _u64p]
+if hasattr(_lib, "xfg_debug_coin_draws"):  # absent from builds older than the device transcript
+    _lib.xfg_debug_coin_draws.argtypes = [C.c_void_p, C.POINTER(C.c_uint32), C.c_uint64, C.c_uint32, C.c_uint32,
+                                          _u64p, _u64p, _u64p, _u64p, C.POINTER(C.c_int)]
 
 
 class XfgStarkError(Exception):
@@ -543,6 +546,24 @@ class XfgBurnMintProver:
         if st:
             raise self._err(st)
         return out
+
+    def debug_coin_draws(self, seed, counter, k, ext=1, reject=(0, 0, 0, 0)):
+        """device transcript draws (xfg_debug_coin_draws): seed = 32 bytes, k <= 64 draws of E by one
+        wave and one at a time, with counters 1..256 force-rejected where `reject` (4 x u64 bits) is
+        set. Returns (wave [k][2], sequential [k][2], counters (wave, seq), ok (wave, seq))"""
+        import numpy as np
+        w = (C.c_uint32 * 8)(*np.frombuffer(bytes(seed), dtype="<u4").tolist())
+        rej = np.array(reject, dtype=np.uint64)
+        ow = np.zeros((k, 2), dtype=np.uint64)
+        osq = np.zeros((k, 2), dtype=np.uint64)
+        ctr = np.zeros(2, dtype=np.uint64)
+        ok = (C.c_int * 2)()
+        st = _lib.xfg_debug_coin_draws(self._ctx, w, counter, k, ext, rej.ctypes.data_as(_u64p),
+                                       ow.ctypes.data_as(_u64p), osq.ctypes.data_as(_u64p),
+                                       ctr.ctypes.data_as(_u64p), ok)
+        if st:
+            raise self._err(st)
+        return ow, osq, (int(ctr[0]), int(ctr[1])), (ok[0], ok[1])
 
     def debug_interpolate(self, evals, n, offset7=False):
         import numpy as np
