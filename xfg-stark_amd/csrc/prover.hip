@@ -342,6 +342,7 @@ struct xfg_ctx {
     uint64_t next_ticket = 1;
     std::map<uint64_t, std::unique_ptr<xfg::Batch>> pending;
     int last_lane = 0;
+    int idle = 0;  // lane workers waiting for a unit
     // batched GPU verification workspace (xfg_verify_batch_gpu)
     struct {
         xfg::HBuf<uint8_t> stage;  // pinned: proof blob + task lists, one DMA
@@ -1050,6 +1051,12 @@ static int unit_size() {
     return v;
 }
 
+// smallest unit a queued unit is split into when lanes would otherwise idle (0: never split)
+static int split_min() {
+    static const int v = std::max(0, env_int("XFG_SPLIT_MIN", 8));
+    return v;
+}
+
 static void copy_unit(Batch* b, int b0, int b1) {
     for (int k = b0; k < b1; k++) {
         ProofJob& j = b->jobs[k];
@@ -1091,12 +1098,30 @@ static void worker_main(xfg_ctx* c, int l) {
                     if (it->lane < 0 || it->lane == l) return true;
                 return false;
             };
+            c->idle++;
             c->qcv.wait(g, [&] { return c->stop || pick(); });
+            c->idle--;
             if (c->stop) return;
             u = *it;
             c->q.erase(it);
             skip = (bool)u.b->err;  // a failed batch drops its remaining units
             L->timing = c->timing;
+            // fewer queued units than idle lanes (the end of a run of batches, or a lone batch):
+            // halve this unit until every idle lane has a share, the halves at the queue's front
+            if (u.lane < 0 && !c->timing && !skip && split_min() > 0) {
+                int avail = 0;
+                for (auto& x : c->q) avail += x.lane < 0;
+                bool pushed = false;
+                while (u.b1 - u.b0 >= 2 * split_min() && avail < c->idle) {
+                    const int mid = u.b0 + (u.b1 - u.b0) / 2;
+                    c->q.push_front(Unit{u.b, mid, u.b1, -1});
+                    u.b->units_left++;
+                    u.b1 = mid;
+                    avail++;
+                    pushed = true;
+                }
+                if (pushed) c->qcv.notify_all();
+            }
         }
         Batch* b = u.b;
         std::exception_ptr e;
