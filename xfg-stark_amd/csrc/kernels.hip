@@ -11,6 +11,7 @@
 //   - FriProver::build_layers: fold-by-8 (apply_drp) and per-layer commitments
 // All arithmetic is 64-bit Goldilocks integer work: HBM/VALU bound, no MFMA.
 #include "kernels.hpp"
+#include "field_dft.hpp"
 #include <algorithm>
 
 namespace xfg {
@@ -855,8 +856,6 @@ struct FoldArgs {
     const u64* alpha7;  // [proof][D]: alpha * 7^-1
     u64* out;           // [proof][D][rows]
     u64 out_stride;
-    u64 winv8[4];  // w_8^-k, k < 4
-    u64 inv8;
     Tables T;
 };
 template <int D>
@@ -866,26 +865,23 @@ __global__ __launch_bounds__(256) void fri_fold_kernel(FoldArgs a) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.rows) return;
     const u64* base = a.vals + (u64)proof * a.val_stride;
-    F v[8];
-    // bit-reversed load for an in-register radix-2 DIT inverse DFT of size 8 (per coordinate:
-    // the twiddles are base-field)
-    const int br[8] = {0, 4, 2, 6, 1, 5, 3, 7};
+    // the size-8 inverse DFT per coordinate (base-field twiddles w_8^-k = powers of two: shifts),
+    // natural order in and out, outputs canonicalised for the Horner adds
+    u64 c[D][8];
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-        const u64 K = i + (u64)br[k] * a.rows;
-        v[k].a = layer_at(base, a.coset_major, a.logn, a.logbeta, K);
-        if constexpr (D == 2) v[k].b = layer_at(base + a.comp_stride, a.coset_major, a.logn, a.logbeta, K);
+        const u64 K = i + (u64)k * a.rows;
+        c[0][k] = layer_at(base, a.coset_major, a.logn, a.logbeta, K);
+        if constexpr (D == 2) c[1][k] = layer_at(base + a.comp_stride, a.coset_major, a.logn, a.logbeta, K);
     }
+    F v[8];
 #pragma unroll
-    for (int s = 0; s < 3; s++) {
-        const int h = 1 << s;
+    for (int d = 0; d < D; d++) {
+        dft_reg<3, true>(c[d]);
 #pragma unroll
-        for (int b = 0; b < 4; b++) {
-            int pos = b & (h - 1), i0 = ((b >> s) << (s + 1)) + pos;
-            u64 w = a.winv8[pos << (2 - s)];
-            F u = v[i0], t = fe_mulb(v[i0 + h], w);
-            v[i0] = fe_add(u, t);
-            v[i0 + h] = fe_sub(u, t);
+        for (int k = 0; k < 8; k++) {
+            if (d == 0) v[k].a = canon(c[d][k]);
+            if constexpr (D == 2) if (d == 1) v[k].b = canon(c[d][k]);
         }
     }
     // y = alpha * 7^-1 * w_D^-i ; Horner
@@ -893,7 +889,13 @@ __global__ __launch_bounds__(256) void fri_fold_kernel(FoldArgs a) {
     F r = v[7];
 #pragma unroll
     for (int j = 6; j >= 0; j--) r = fe_add(fe_mul(r, y), v[j]);
-    r = fe_mulb(r, a.inv8);
+    // 1/8 = 2^-3 = 2^189 = -2^93
+#pragma unroll
+    for (int d = 0; d < D; d++) {
+        const u64 x = gl_neg(mul_pow2<93>(r.c(d)));
+        if (d == 0) r.a = x;
+        if constexpr (D == 2) if (d == 1) r.b = x;
+    }
 #pragma unroll
     for (int c = 0; c < D; c++) a.out[((u64)proof * D + c) * a.out_stride + i] = r.c(c);
 }
@@ -905,9 +907,6 @@ void launch_fri_fold(const u64* vals, u64 val_stride, u64 comp_stride, bool cose
     a.logn = logn; a.logbeta = logbeta; a.rows = rows; a.logD = logD; a.alpha7 = alpha7; a.out = out;
     a.out_stride = out_stride;
     a.T = T;
-    u64 w8inv = gl_inv(gl_root(3));
-    for (int k = 0; k < 4; k++) a.winv8[k] = gl_pow(w8inv, k);
-    a.inv8 = gl_inv(8);
     int threads = rows < 256 ? (int)rows : 256;
     dim3 g((unsigned)((rows + threads - 1) / threads), npoly);
     if (ext == 2) hipLaunchKernelGGL(fri_fold_kernel<2>, g, dim3(threads), 0, s, a);
