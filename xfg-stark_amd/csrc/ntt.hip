@@ -49,15 +49,27 @@ __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, u32 voff, u32 s
     __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)voff, (int)soff, 0);
 }
 
-// LDS tile: row `seq` of length S at seq * PITCH; element i at i + (i >> 4). The pad word per 16
-// elements makes the stride-16 stores of a first step conflict-free; the odd pitch does the same
-// for lanes walking across rows.
-__host__ __device__ constexpr int row_pitch(int S) { return S + S / 16 + 1; }
-__device__ __forceinline__ int phys(int i) { return i + (i >> 4); }
-// phys(j + o) for an offset o that is a compile-time constant after unrolling: a multiple of 16
+// LDS tile: row `seq` of length S at seq * PITCH; element i at i + (i >> P), one pad word per 2^P
+// elements, P = log2 elements per thread (4 or 5). The pad word makes the stride-2^P stores of a
+// full-radix first step (lanes along a row, 2^P contiguous outputs each) conflict-free: 16 lanes
+// land on 16 different 8-byte bank pairs. The pitch does the same for lanes walking across rows:
+// a 16-lane group spans 2^L rows and 16 / 2^L consecutive elements, so the pitch must be an odd
+// multiple of 16 / 2^L mod 16 (radix 16: odd; radix 32 with 8-row tiles, pass B at n = 2^20: 2 mod
+// 4 -- the odd pitch there cost 2-way conflicts on every last-step read, and the pad per 16 on
+// every first-step write, 14.8 M conflict cycles per configs[4] trace LDE).
+// L = log2 of the tile's row count (the kernel's maximum; a smaller tile only uses fewer rows).
+__host__ __device__ constexpr int row_pitch(int S, int P = 4, int L = 4) {
+    return P == 4 ? S + S / 16 + 1 : S + (S >> P) + ((L >= 4 || L <= 0) ? 1 : (16 >> L));
+}
+template <int P>
+__device__ __forceinline__ int phys(int i) { return i + (i >> P); }
+// phys(j + o) for an offset o that is a compile-time constant after unrolling: a multiple of 2^P
 // splits off as a constant (the LDS instruction's immediate offset), so the per-lane index
 // phys(j) is computed once per group instead of once per element
-__device__ __forceinline__ int phys2(int j, int o) { return (o & 15) == 0 ? phys(j) + o + (o >> 4) : phys(j + o); }
+template <int P>
+__device__ __forceinline__ int phys2(int j, int o) {
+    return (o & ((1 << P) - 1)) == 0 ? phys<P>(j) + o + (o >> P) : phys<P>(j + o);
+}
 
 __device__ __forceinline__ u64 tw_get(const Tables& T, int k, u64 e, bool inv) {
     const u64 M = 1ULL << T.LM;
@@ -131,10 +143,12 @@ struct Plan {
 // Whole DFT of every sequence: the first step loads with ldg (global), middle steps run in the
 // LDS tile, the last step stores with stg (global). A one-step DFT goes global -> global.
 // stg(q, seq, base, stride, v) stores group q's outputs; pf as in stockham, for the last step
+constexpr int NT_LOG2(int nt) { return nt <= 1 ? 0 : 1 + NT_LOG2(nt / 2); }
 template <int LOGS, int LOGE, bool INV, bool FIRST_SEQ_FAST, int NT, class LDG, class STG, class PF>
 __device__ __forceinline__ void pass_dft(u64* tile, int lognseq, const u64* ltw, LDG ldg, STG stg, PF pf) {
     using PL = Plan<LOGS, LOGE>;
-    constexpr int PITCH = row_pitch(1 << LOGS), E = 1 << LOGE;
+    constexpr int L = NT_LOG2(NT) + LOGE - LOGS;
+    constexpr int PITCH = row_pitch(1 << LOGS, LOGE, L), E = 1 << LOGE;
     auto nopf = [](int, int, int, int) {};
     if constexpr (PL::NSTEP == 1) {
         stockham<LOGS, PL::FIRST_LOGR, LOGE, INV, FIRST_SEQ_FAST, false, NT>(lognseq, 1, ltw, ldg, stg, pf);
@@ -146,8 +160,8 @@ __device__ __forceinline__ void pass_dft(u64* tile, int lognseq, const u64* ltw,
                 for (int r = 0; r < (1 << PL::FIRST_LOGR); r++) {
                     // full-radix first step: base = R j, stride 1 -> the R outputs are contiguous
                     // (a multiple of 16 elements: the pad words fall at fixed offsets)
-                    if constexpr (PL::FIRST_LOGR >= 4) row[phys(base) + r + (r >> 4)] = v[r];
-                    else row[phys(base + r * stride)] = v[r];
+                    if constexpr (PL::FIRST_LOGR >= 4) row[phys<LOGE>(base) + r + (r >> LOGE)] = v[r];
+                    else row[phys<LOGE>(base + r * stride)] = v[r];
                 }
             },
             nopf);
@@ -156,18 +170,18 @@ __device__ __forceinline__ void pass_dft(u64* tile, int lognseq, const u64* ltw,
 #pragma unroll
         for (int st = 1; st < PL::NSTEP - 1; st++) {
             stockham<LOGS, LOGE, LOGE, INV, true, true, NT>(
-                lognseq, Ns, ltw, [&](int seq, int j, int o) { return tile[seq * PITCH + phys2(j, o)]; },
+                lognseq, Ns, ltw, [&](int seq, int j, int o) { return tile[seq * PITCH + phys2<LOGE>(j, o)]; },
                 [&](int, int seq, int base, int stride, u64* v) {
                     u64* row = tile + seq * PITCH;
 #pragma unroll
-                    for (int r = 0; r < E; r++) row[phys2(base, r * stride)] = v[r];
+                    for (int r = 0; r < E; r++) row[phys2<LOGE>(base, r * stride)] = v[r];
                 },
                 nopf);
             __syncthreads();
             Ns <<= LOGE;
         }
         stockham<LOGS, PL::LAST_LOGR, LOGE, INV, true, false, NT>(
-            lognseq, Ns, ltw, [&](int seq, int j, int o) { return tile[seq * PITCH + phys2(j, o)]; }, stg, pf);
+            lognseq, Ns, ltw, [&](int seq, int j, int o) { return tile[seq * PITCH + phys2<LOGE>(j, o)]; }, stg, pf);
         __syncthreads();
     }
 }
@@ -215,7 +229,8 @@ __device__ __forceinline__ void xcd_block(bool on, int& bx, int& by) {
 // LDS, one block per CU: 16 columns per tile even at R = 1024)
 template <int LOGR, bool INV, int LOGT, int LOGE>
 __global__ __launch_bounds__(1 << LOGT, (1 << (10 - LOGT)) >> (LOGE - 4)) void ntt_pass_a(NttArgs a) {
-    constexpr int R = 1 << LOGR, PITCH = row_pitch(R), RR = Plan<LOGR, LOGE>::LAST_R, NT = 1 << LOGT;
+    constexpr int R = 1 << LOGR, PITCH = row_pitch(R, LOGE, LOGT + LOGE - LOGR), RR = Plan<LOGR, LOGE>::LAST_R,
+                  NT = 1 << LOGT;
     extern __shared__ u64 lds[];
     const int logTC = (a.logC < LOGT + LOGE - LOGR) ? a.logC : LOGT + LOGE - LOGR;
     const int TC = 1 << logTC;
@@ -354,7 +369,7 @@ __global__ __launch_bounds__(1 << LOGT) void ntt_pass_b(NttArgs a) {
     const int logTR = (a.logR < LOGT + LOGE - LOGC) ? a.logR : LOGT + LOGE - LOGC;
     const int TR = 1 << logTR;
     u64* tile = lds;
-    u64* ltw = lds + TR * row_pitch(C);
+    u64* ltw = lds + TR * row_pitch(C, LOGE, LOGT + LOGE - LOGC);
     int bx, by;
     xcd_block(a.xcd & 2, bx, by);
     const int pt = by, k10 = bx * TR;
@@ -631,8 +646,8 @@ static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
     const int logTC = a.logC < ltA + eA - a.logR ? a.logC : ltA + eA - a.logR;
     const int logTR = a.logR < ltB + eB - a.logC ? a.logR : ltB + eB - a.logC;
     const int ncos = inv ? 1 : (1 << a.logbeta);
-    size_t lds_a = ((size_t)(1 << logTC) * row_pitch(R) + 2 * R) * sizeof(u64);
-    size_t lds_b = ((size_t)(1 << logTR) * row_pitch(C) + C) * sizeof(u64);
+    size_t lds_a = ((size_t)(1 << logTC) * row_pitch(R, eA, ltA + eA - a.logR) + 2 * R) * sizeof(u64);
+    size_t lds_b = ((size_t)(1 << logTR) * row_pitch(C, eB, ltB + eB - a.logC) + C) * sizeof(u64);
     dim3 ga(C >> logTC, npoly * ncos), gb(R >> logTR, npoly * ncos);
     // tile rows narrower than 16 words (a 128 B line) in the scattered writes: pass A stores TC
     // consecutive words per row, pass B TR (XFG_NTT_XCD=0 disables, for A/B runs)
