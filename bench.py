@@ -151,7 +151,7 @@ def config5(prover, batch=4, calls=8, depth=4):
     saved = prover._options
     prover._options = o
     try:
-        prover.prepare(batch, n5)
+        prover.prepare(batch, n5, buffers=depth)
         kws = [synthetic.burn_inputs(50_000 + i) for i in range(batch)]
         pend = []
         t = time.perf_counter()
@@ -262,7 +262,9 @@ def main():
     prover = xfgstark.XfgBurnMintProver(device=gpu)
     n = 1 << args.log_n
     per = args.per_gpu
-    prover.prepare(per, n)  # workspace allocation + code-object load (setup, not a proving step)
+    # workspace allocation, code-object load and one host output buffer per batch in flight (setup,
+    # not a proving step)
+    prover.prepare(per, n, buffers=args.depth)
 
     # synthetic inputs for every step, generated before the timed region (rank 0 holds the
     # batches; for N > 1 they are packed into HBM and scattered over RCCL inside each step)

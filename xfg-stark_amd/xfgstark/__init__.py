@@ -7,6 +7,7 @@ for gfx950); there is no CPU fallback: if the library is missing this module fai
 without a GPU the prover constructor raises.
 """
 import ctypes as C
+import mmap
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -335,6 +336,12 @@ def exported_symbols():
     return [name for name in dir(_lib)]
 
 
+def _anon_map(size):
+    """private anonymous mapping (the default mmap.mmap(-1, n) is MAP_SHARED: shmem pages, slower
+    to fault and to write than the private pages malloc hands out)"""
+    return mmap.mmap(-1, size, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+
+
 class PendingBatch:
     """a submitted batch (XfgBurnMintProver.submit_batch); result() -> list of StarkProof | XfgStarkError"""
 
@@ -468,19 +475,32 @@ class XfgBurnMintProver:
         return PendingBatch(self, ticket.value, buf, base, cap, outs, lens, sts)
 
     def _take_buffer(self, size):
-        # output buffers are recycled (a fresh create_string_buffer zero-fills megabytes per batch)
+        # output buffers are recycled. A new one is an anonymous mapping, not create_string_buffer:
+        # that zero-fills the whole bound (64 x 0.7 MB at n = 2^16) on the calling thread -- 11 ms
+        # of page faults per batch, during which the next batch could not be submitted. The
+        # mapping's pages are faulted in by the workers' proof copies instead, once.
         free = self.__dict__.setdefault("_free", [])
         for i, b in enumerate(free):
             if C.sizeof(b) >= size:
                 return free.pop(i)
-        return C.create_string_buffer(size)
+        return (C.c_char * size).from_buffer(_anon_map(size))
 
-    def prepare(self, count, trace_length=64):
-        """allocate workspaces for batches of `count` proofs of this shape (setup, untimed)"""
+    def prepare(self, count, trace_length=64, buffers=0):
+        """allocate workspaces for batches of `count` proofs of this shape (setup, untimed), and
+        `buffers` host output buffers for submit_batch, their pages touched now -- as many as the
+        caller keeps batches in flight, so steady-state submissions allocate nothing"""
         o = self._options._c()
         st = _lib.xfg_prepare(self._ctx, count, trace_length, C.byref(o))
         if st:
             raise self._err(st)
+        if buffers:
+            size = _lib.xfg_proof_size_bound(trace_length, C.byref(o)) * count
+            free = self.__dict__.setdefault("_free", [])
+            have = sum(1 for b in free if C.sizeof(b) >= size)
+            for _ in range(max(0, buffers - have)):
+                b = (C.c_char * size).from_buffer(_anon_map(size))
+                C.memset(b, 0, size)  # fault the pages in at setup
+                free.append(b)
 
     # ---- instrumentation
     def set_timing(self, on=True):
