@@ -55,11 +55,12 @@ def test_lde_kernel_matches_oracle(prover, n, blowup):
         assert [int(v) for v in got[p]] == want
 
 
-@pytest.mark.parametrize("n,blowup", [(1 << 18, 2), (1 << 22, 2)])
+@pytest.mark.parametrize("n,blowup", [(1 << 18, 2), (1 << 22, 2), (1 << 20, 16), (1 << 22, 4)])
 def test_lde_kernel_tile_paths_match_oracle(prover, n, blowup):
     """the remaining four-step shapes: 2^18 (R = 256 narrow tiles, C = 1024 with 512-thread pass B
     tiles) and 2^22 (R = 1024 wide 1024-thread pass A, C = 4096 narrow pass B), one polynomial,
-    compared as arrays"""
+    compared as arrays; 2^20 x 16 (configs[4]) and 2^22 x 4: 2^24 points, past the four-step
+    tables (running-product twiddles, standalone pass tables)"""
     rng = np.random.default_rng(n + 7)
     coef = rng.integers(0, P, size=(1, n), dtype=np.uint64)
     got = np.asarray(prover.debug_lde(coef, n, blowup))[0]

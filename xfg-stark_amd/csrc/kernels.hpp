@@ -30,9 +30,14 @@ struct DeepParams {
 // 7^j2 w_N^(j2 (t + beta k1)) at [t][k1][j2], inv[logn] holds w_n^-(j2 k1) / n at [k1][j2];
 // nullptr -> the kernels form them as running products
 constexpr int FOURSTEP_MAX_LOG = 22;
+// forward sizes past FOURSTEP_MAX_LOG (configs[4]: 2^20 x 16 = 2^24 points, a 128 MB table) keep the
+// running-product four-step twiddles but still get the small per-size pass tables (w_R^i, w_C^i and
+// the coset pre-factors, R + C + beta R entries) as one contiguous block: pass_fwd[logn][logbeta]
+constexpr int PASS_MAX_LOG = 24;
 struct FourStep {
     const u64* fwd[FOURSTEP_MAX_LOG + 1][5] = {};
     const u64* inv[FOURSTEP_MAX_LOG + 1] = {};
+    const u64* pass_fwd[PASS_MAX_LOG + 1][5] = {};
 };
 struct Tables {
     const u64* tw;     // tw[e] = w_{2^LM}^e, e < 2^LM
@@ -49,6 +54,9 @@ void launch_lde(const u64* coef, u64 coef_stride, u64* out, u64* scratch, int np
 // entries of the four-step table for (logn, logbeta) (inverse: logbeta = -1), and its generator
 u64 fourstep_size(int logn, int logbeta);
 void build_fourstep(u64* out, int logn, int logbeta, const Tables& T, hipStream_t s);
+// the pass tables alone (forward, for sizes without a four-step table): entries and generator
+u64 pass_tables_size(int logn, int logbeta);
+void build_pass_tables(u64* out, int logn, int logbeta, const Tables& T, hipStream_t s);
 // field-primitive self test (xfg_debug_field): op 0 mul, 1 add, 2 sub, 3 canon(a), 4 a * 2^b,
 // 5 fold(a, (u32)b), 6 sub_weak(a, b), 7 add_w(a, b) (the NTT butterfly add, b < p)
 void launch_field_op(int op, const u64* a, const u64* b, u64* out, u64 count, hipStream_t s);

@@ -198,6 +198,7 @@ struct NttArgs {
     u64 scale;    // inverse: n^-1
     u64 keep;     // inverse: coefficients written
     const u64* t4;  // four-step twiddle table (FourStep) or nullptr
+    const u64* pt;  // pass tables: w_R^(+-i) [R], w_C^(+-i) [C], forward coset pre-factors [beta][R]; or nullptr
     int xcd;        // 1: XCD-contiguous block order (see xcd_block)
     int tq_b;       // forward: pass B applies the four-step twiddles as it loads (ntt_pass_a_cos)
     Tables T;
@@ -245,12 +246,11 @@ __global__ __launch_bounds__(1 << LOGT, (1 << (10 - LOGT)) >> (LOGE - 4)) void n
     const u64 n = 1ULL << a.logn;
     const int logN = a.logn + a.logbeta;
     const u64 maskN = (1ULL << logN) - 1;
-    if (a.t4) {
-        // contiguous per-size tables behind the four-step table (build_fourstep): coalesced loads
-        const u64* pt4 = a.t4 + fourstep_main(a.logn, INV ? -1 : a.logbeta);
+    if (a.pt) {
+        // contiguous per-size tables (behind the four-step table, or standalone): coalesced loads
         for (int i = threadIdx.x; i < R; i += NT) {
-            ltw[i] = pt4[i];
-            if (!INV) pre[i] = pt4[R + (1 << a.logC) + t * R + i];
+            ltw[i] = a.pt[i];
+            if (!INV) pre[i] = a.pt[R + (1 << a.logC) + t * R + i];
         }
     } else {
         for (int i = threadIdx.x; i < R; i += NT) {
@@ -272,10 +272,25 @@ __global__ __launch_bounds__(1 << LOGT, (1 << (10 - LOGT)) >> (LOGE - 4)) void n
     // so the table latency hides behind them; one multiply per element instead of two
     constexpr int PERL = (1 << LOGE) / RR;
     u64 tq[PERL][RR];
+    // without a table: the running product's seed and step (and 7^j2), gathered by pf as well so
+    // that their latency also hides behind the last step's loads and butterflies
+    u64 wq[PERL], sq[PERL], p7q[PERL];
     const u64* tab = a.t4 ? a.t4 + (INV ? 0 : ((u64)t << a.logn)) + col0 : nullptr;
     const auto rtab = buf_rsrc(tab ? tab : y);
     auto pf = [&](int q, int seq, int base, int stride) {
-        if (!tab) return;
+        if (!tab) {
+            const u64 j2 = col0 + seq;
+            if (INV) {
+                wq[q] = tw_get(a.T, a.logn, (j2 * (u64)base) & (n - 1), true);
+                sq[q] = tw_get(a.T, a.logn, (j2 * (u64)stride) & (n - 1), true);
+            } else {
+                // 7^j2 w_N^(j2 (t + beta base)); step w_N^(j2 beta stride) = w_n^(j2 stride)
+                p7q[q] = a.T.pow7[j2];
+                wq[q] = tw_get(a.T, logN, (j2 * ((u64)t + ((u64)base << a.logbeta))) & maskN, false);
+                sq[q] = tw_get(a.T, a.logn, (j2 * (u64)stride) & (n - 1), false);
+            }
+            return;
+        }
         const u32 vo = (((u32)base << a.logC) + seq) * 8;
 #pragma unroll
         for (int r = 0; r < RR; r++) tq[q][r] = buf_ld(rtab, vo, ((u32)(r * stride) << a.logC) * 8);
@@ -288,15 +303,8 @@ __global__ __launch_bounds__(1 << LOGT, (1 << (10 - LOGT)) >> (LOGE - 4)) void n
             for (int r = 0; r < RR; r++) buf_st(ry, vo, ((u32)(r * stride) << a.logC) * 8, gl_mul(v[r], tq[q][r]));
             return;
         }
-        u64 w, step;
-        if (INV) {
-            w = tw_get(a.T, a.logn, (j2 * (u64)base) & (n - 1), true);
-            step = tw_get(a.T, a.logn, (j2 * (u64)stride) & (n - 1), true);
-        } else {
-            // 7^j2 w_N^(j2 (t + beta base)); step w_N^(j2 beta stride) = w_n^(j2 stride)
-            w = gl_mul(a.T.pow7[j2], tw_get(a.T, logN, (j2 * ((u64)t + ((u64)base << a.logbeta))) & maskN, false));
-            step = tw_get(a.T, a.logn, (j2 * (u64)stride) & (n - 1), false);
-        }
+        u64 w = INV ? wq[q] : gl_mul(p7q[q], wq[q]);
+        const u64 step = sq[q];
 #pragma unroll
         for (int r = 0; r < RR; r++) {
             y[((u64)(base + r * stride) << a.logC) + j2] = gl_mul(v[r], w);
@@ -327,7 +335,7 @@ __global__ __launch_bounds__(256, 3) void ntt_pass_a_cos(NttArgs a) {
     const int poly = blockIdx.y, col0 = blockIdx.x * TC;
     const u64 n = 1ULL << a.logn;
     const int beta = 1 << a.logbeta;
-    const u64* pt4 = a.t4 + fourstep_main(a.logn, a.logbeta);
+    const u64* pt4 = a.pt;
     const u64* pre_all = pt4 + R + (1 << a.logC);  // [t][R]
     for (int i = threadIdx.x; i < R; i += NT) {
         ltw[i] = pt4[i];
@@ -374,8 +382,8 @@ __global__ __launch_bounds__(1 << LOGT) void ntt_pass_b(NttArgs a) {
     xcd_block(a.xcd & 2, bx, by);
     const int pt = by, k10 = bx * TR;
     const u64 n = 1ULL << a.logn;
-    if (a.t4) {
-        const u64* pt4 = a.t4 + fourstep_main(a.logn, INV ? -1 : a.logbeta) + (1 << a.logR);
+    if (a.pt) {
+        const u64* pt4 = a.pt + (1 << a.logR);
         for (int i = threadIdx.x; i < C; i += NT) ltw[i] = pt4[i];
     } else {
         for (int i = threadIdx.x; i < C; i += NT) ltw[i] = tw_get(a.T, LOGC, i, INV);
@@ -591,6 +599,18 @@ __global__ void pass_tables_kernel(u64* out, int logn, int logbeta, int logR, in
         out[i] = gl_mul(T.pow7[j << logC], tw_get(T, logR + logbeta, (t * j) & ((1ULL << (logR + logbeta)) - 1), false));
     }
 }
+u64 pass_tables_size(int logn, int logbeta) {
+    int logR, logC;
+    ntt_split(logn, logR, logC);
+    return (1ULL << logR) + (1ULL << logC) + (logbeta >= 0 ? (1ULL << (logR + logbeta)) : 0);
+}
+void build_pass_tables(u64* out, int logn, int logbeta, const Tables& T, hipStream_t s) {
+    int logR, logC;
+    ntt_split(logn, logR, logC);
+    const u64 cnt = pass_tables_size(logn, logbeta);
+    hipLaunchKernelGGL(pass_tables_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s, out, logn, logbeta,
+                       logR, logC, T);
+}
 __host__ __device__ u64 fourstep_main(int logn, int logbeta) { return 1ULL << (logn + (logbeta > 0 ? logbeta : 0)); }
 u64 fourstep_size(int logn, int logbeta) {
     int logR, logC;
@@ -701,6 +721,8 @@ void launch_lde(const u64* coef, u64 coef_stride, u64* out, u64* scratch, int np
         a.logbeta = logbeta;
         a.T = T;
         a.t4 = (T.fs && logn <= FOURSTEP_MAX_LOG && logbeta <= 4) ? T.fs->fwd[logn][logbeta] : nullptr;
+        a.pt = a.t4 ? a.t4 + fourstep_main(logn, logbeta)
+                    : ((T.fs && logn <= PASS_MAX_LOG && logbeta <= 4) ? T.fs->pass_fwd[logn][logbeta] : nullptr);
         ntt_run(a, std::min(chunk, npoly - p0), false, s);
     }
 }
@@ -720,6 +742,7 @@ void launch_interpolate(const u64* evals, u64 in_stride, u64* out, u64 out_strid
     a.T = T;
     a.scale = gl_inv(1ULL << logn);
     a.t4 = (T.fs && logn <= FOURSTEP_MAX_LOG) ? T.fs->inv[logn] : nullptr;
+    a.pt = a.t4 ? a.t4 + fourstep_main(logn, -1) : nullptr;
     ntt_run(a, npoly, true, s);
 }
 

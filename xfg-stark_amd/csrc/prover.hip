@@ -220,6 +220,7 @@ struct TablesHost {
     std::map<int, DBuf<u64>> ce_div;  // constraint divisor tables per log2(trace length)
     FourStep fs;                      // four-step twiddle tables (pointers into four_buf)
     std::map<int, DBuf<u64>> four_buf;
+    std::map<int, DBuf<u64>> pass_buf;  // standalone forward pass tables (fs.pass_fwd)
 };
 
 // Data-independent constraint divisors on the CE domain x_i = 7 w_2n^i (i = 2m + par), laid out
@@ -404,6 +405,7 @@ static Tables tables_of(xfg_ctx* c) {
 static bool fourstep_ready(xfg_ctx* c, int logn, int logbeta) {
     const FourStep& f = c->tables.fs;
     if (logn + logbeta <= FOURSTEP_MAX_LOG && !f.fwd[logn][logbeta]) return false;
+    if (logn + logbeta > FOURSTEP_MAX_LOG && logn <= PASS_MAX_LOG && !f.pass_fwd[logn][logbeta]) return false;
     for (int l = 3; l <= std::min(logn + 1, FOURSTEP_MAX_LOG); l++)
         if (!f.inv[l]) return false;
     return true;
@@ -421,6 +423,12 @@ static void ensure_fourstep(xfg_ctx* c, int logn, int logbeta) {
     };
     FourStep& f = c->tables.fs;
     if (logn + logbeta <= FOURSTEP_MAX_LOG && !f.fwd[logn][logbeta]) f.fwd[logn][logbeta] = build(logn, logbeta);
+    if (logn + logbeta > FOURSTEP_MAX_LOG && logn <= PASS_MAX_LOG && !f.pass_fwd[logn][logbeta]) {
+        DBuf<u64>& b = c->tables.pass_buf[logn * 8 + logbeta];
+        b.ensure(pass_tables_size(logn, logbeta));
+        build_pass_tables(b.p, logn, logbeta, T, 0);
+        f.pass_fwd[logn][logbeta] = b.p;
+    }
     for (int l = 3; l <= std::min(logn + 1, FOURSTEP_MAX_LOG); l++)
         if (!f.inv[l]) f.inv[l] = build(l, -1);
     HIPCHK(hipStreamSynchronize(0));
@@ -1282,6 +1290,7 @@ void xfg_ctx_destroy(xfg_ctx* c) {
     c->tables.ipow7.release();
     for (auto& kv : c->tables.ce_div) kv.second.release();
     for (auto& kv : c->tables.four_buf) kv.second.release();
+    for (auto& kv : c->tables.pass_buf) kv.second.release();
     delete c;
 }
 
