@@ -59,7 +59,7 @@ def scatter_inputs(all_inputs, rank, world, per_rank, device, dist, packed=None)
     """rank 0's batch inputs -> this rank's shard (list of prove kwargs). `packed` = the batch
     already packed into a [world, per_rank, REC] uint8 device tensor on rank 0 (resident in HBM)."""
     import torch
-    if world == 1:
+    if dist is None:
         return all_inputs
     if rank == 0:
         if packed is None:
@@ -79,7 +79,7 @@ def gather_proofs(proofs, rank, world, per_rank, device, dist):
     pinned buffer: the views stay valid until the next call)"""
     import numpy as np
     import torch
-    if world == 1:
+    if dist is None:
         return proofs
     lens = np.array([len(p) for p in proofs], dtype=np.int64)
     hdr = 8 * per_rank
@@ -241,6 +241,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-config5", action="store_true", help="skip the configs[4] side measurement")
     ap.add_argument("--depth", type=int, default=6, help="batches in flight (pipelined submission)")
+    ap.add_argument("--dist", action="store_true",
+                    help="run the scatter / gather collectives even at world size 1 (exercises the RCCL "
+                         "path on a one-GPU box; launch with torch.distributed.run)")
     args = ap.parse_args()
 
     import torch
@@ -252,7 +255,7 @@ def main():
     # share the visible GPUs round-robin and the scatter / gather tensors stay on the host
     backend = os.environ.get("XFG_DIST_BACKEND", "nccl")
     gpu = local_rank % max(1, torch.cuda.device_count()) if backend != "nccl" else local_rank
-    if world > 1:
+    if world > 1 or args.dist:
         import torch.distributed as dist
         torch.cuda.set_device(gpu)
         dist.init_process_group(backend)
@@ -272,7 +275,7 @@ def main():
     batches = [[synthetic.burn_inputs(k * per * world + i) for i in range(per * world)] if rank == 0 else None
                for k in range(total_steps)]
     packed = None
-    if world > 1:
+    if dist is not None:
         packed = [torch.from_numpy(pack_inputs(b)).to(device).view(world, per, REC) if rank == 0 else None
                   for b in batches]
 
@@ -307,6 +310,9 @@ def main():
     el = float(el_t.item())
     if rank == 0:
         assert out is not None and len(out) == per * world
+        if args.dist:  # the collective path's output: the gathered proofs of the last step, in order
+            want = [p.to_bytes() for p in prover.prove_batch(batches[-1], trace_length=n)]
+            assert [bytes(x) for x in out] == want, "gathered proofs differ from a direct prove_batch"
     pipe_ms, pipe_sets, pipe_polys = prover.lde_probe(False)
 
     # one synchronous batch call (no pipelining), for reference

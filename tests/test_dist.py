@@ -136,3 +136,23 @@ def test_gather_proofs_device_branch():
     other = {"size": torch.tensor([size], dtype=torch.int64), "payload": torch.from_numpy(pay)}
     out = bench.gather_proofs(mine, 0, 2, per, torch.device("cuda", 0), _LoopbackDist(other))
     assert [bytes(x) for x in out] == mine + theirs
+
+
+@pytest.mark.gpu
+def test_bench_rccl_collectives_one_rank():
+    """bench.py's exchange step over RCCL itself (backend nccl: device tensors, scatter of packed
+    inputs, length all-reduce, padded gather, pinned D2H of the gathered proofs), one rank on the
+    one-GPU box through torch.distributed.run -- the path the driver's multi-GPU runs take. bench.py
+    --dist checks that the gathered proofs equal a direct prove_batch of the same inputs."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", "1", "--steps", "2", "--warmup", "1", "--per-gpu", "8", "--depth", "2",
+           "--no-cpu-baseline", "--no-config5", "--dist"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 1 and line["steps"] == 2 and line["value"] > 0
