@@ -7,8 +7,11 @@ gathers the proof bytes back over RCCL (torch.distributed "nccl" backend), the o
 step of the path; each rank proves its shard with libxfgstark.so (weak scaling).
 
 Prints ONE JSON line (rank 0) with `roofline` (trace-LDE kernel pair, HIP-event timed on the
-prover's stream) and `cpu_baseline` (the oracle C restatement, 1 thread, faithful per-row
-Keccak mode, bounded sample).
+prover's stream), `whole_proof` (SURVEY 8(d)'s per-proof algorithmic bytes x proofs/s against the
+HBM peak), `verified` (every proof of the last timed step, gathered on rank 0, accepted by the GPU
+batch verifier against its statement -- the run fails otherwise), `verify` (batch-verify
+throughput, GPU vs host threads) and `cpu_baseline` (the oracle C restatement on the host cores:
+1 thread in the reference-faithful per-row Keccak mode, and all cores with OpenMP).
 """
 import argparse
 import json
@@ -140,16 +143,19 @@ def pipelined_steps(submit_fn, collect_fn, batches, rank, world, per_rank, devic
     return out
 
 
-def config5(prover, batch=4, calls=8, depth=4):
+def config5(prover, gpu, batch=4, calls=8, depth=4):
     """side measurement of BASELINE configs[4]: 2^20-step trace, blowup 16, 96-bit class options
     (quadratic extension, 24 queries, grinding 4), batches of `batch` proofs per call on this GPU,
-    `depth` calls in flight"""
+    `depth` calls in flight; the trace LDE (7 columns, one proof) against the HBM roofline with
+    SURVEY 8(d)'s B_LDE = 8 w (n + N) = 998,244,352 B, and the device memory the shape adds"""
+    import torch
     import xfgstark
     n5 = 1 << 20
     o = xfgstark.ProofOptions.reference()
     o.field_extension, o.blowup_factor, o.num_queries = 2, 16, 24
     saved = prover._options
     prover._options = o
+    free0 = torch.cuda.mem_get_info(gpu)[0]
     try:
         prover.prepare(batch, n5, buffers=depth)
         kws = [synthetic.burn_inputs(50_000 + i) for i in range(batch)]
@@ -163,14 +169,29 @@ def config5(prover, batch=4, calls=8, depth=4):
             res = pend.pop(0).result()
         dt = time.perf_counter() - t
         assert all(not isinstance(r, Exception) for r in res)
+        used = free0 - torch.cuda.mem_get_info(gpu)[0]
         lde_ms = prover.bench_lde(1, n5, 16, 5)
     finally:
         prover._options = saved
+    lde_b = 8 * WIDTH * (n5 + 16 * n5)
+    gbps = lde_b / (lde_ms * 1e-3) / 1e9
+    pmc, src = pmc_record(1, n5, 16)
     return {"workload": "configs[4]: 2^20-step trace, blowup 16, quadratic extension, 24 queries, grinding 4",
             "proofs_per_call": batch, "proofs_per_s": round(batch * calls / dt, 2),
             "ms_per_proof": round(dt / (batch * calls) * 1e3, 3), "proof_bytes": len(res[0]),
-            "trace_lde_ms": round(lde_ms, 3),
-            "trace_lde_GBps": round(8 * WIDTH * (n5 + 16 * n5) / (lde_ms * 1e-3) / 1e9, 1)}
+            "trace_lde_ms": round(lde_ms, 3), "trace_lde_bytes": lde_b,
+            "trace_lde_GBps": round(gbps, 1), "trace_lde_frac": round(gbps / PEAK_HBM_GBS, 4),
+            "trace_lde_traffic": pmc["traffic_bytes"] if pmc else None, "traffic_source": src,
+            "device_bytes_added": int(used), "proofs_in_flight": batch * depth}
+
+
+def whole_proof_line(proofs_per_s, n, world):
+    b = whole_proof_bytes(n, BLOWUP)
+    achieved = proofs_per_s * b / 1e9
+    return {"bytes_per_proof": b, "achieved_GBps": round(achieved, 1), "peak": PEAK_HBM_GBS * world,
+            "frac": round(achieved / (PEAK_HBM_GBS * world), 4),
+            "note": "SURVEY 8(d) whole-proof algorithmic bytes (each stage reads its inputs and writes its "
+                    "outputs once) x proofs/s, against the HBM peak of all GPUs"}
 
 
 def in_pipeline(ms, sets, polys, n):
@@ -186,7 +207,7 @@ def pmc_record(per, n, blowup):
     scripts/profile_round.sh: FETCH_SIZE x2 + WRITE_SIZE and SQ_INSTS_VALU, separate rocprofv3 --pmc
     runs) and its path, or (None, None)"""
     import glob
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "lde_pmc.json")), reverse=True):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "lde_pmc*.json")), reverse=True):
         d = json.load(open(f))
         if (d.get("count"), d.get("n"), d.get("blowup")) == (per, n, blowup):
             return d, os.path.relpath(f, ROOT)
@@ -209,25 +230,105 @@ def valu_roofline(rec, lde_ms, outputs):
             "valu_busy_pct": [rec.get("valu_busy_pct_pass_a"), rec.get("valu_busy_pct_pass_b")]}
 
 
+def whole_proof_bytes(n, beta, w=WIDTH, e=8, c=2, fold=8, rem_deg=31):
+    """SURVEY.md 8(d) notes: per-proof algorithmic HBM bytes, every stage reading its inputs once and
+    writing its outputs once (c = 2 composition columns as SURVEY prices it; 221.2 MB at configs[2])"""
+    b, N, nce = 8, n * beta, c * n
+    tot = 2 * b * w * n + b * w * (n + N) + (b * w * N + 32 * N) + 64 * N  # interpolate, LDE, leaves, tree
+    tot += (b * w * nce + e * nce) + 2 * e * nce + e * c * (n + N) + (e * c * N + 32 * N) + 64 * N
+    tot += (b * w + e * c) * n + e * n + e * (n + N)  # DEEP combine + DEEP LDE
+    D = N
+    while D > (rem_deg + 1) * beta:  # FRI layers
+        tot += e * D + 32 * D // fold + 64 * D // fold + e * D // fold
+        D //= fold
+    return tot
+
+
+def host_facts():
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": aff,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
 def cpu_baseline(seconds=10.0):
-    """oracle C restatement, single thread, faithful mode (per-row Keccak like the reference)"""
+    """the oracle C restatement (oracle/liboracle.so) on this host's cores, two modes:
+    (i) 1 thread, faithful per-row Keccak recomputation like the reference (src/burn_mint_air.rs:264,376;
+    Winterfell built without `concurrent`, SURVEY 0.1) -- the reference-faithful figure, `value`;
+    (ii) all cores (OMP_NUM_THREADS, else the CPUs this process may run on) with OpenMP, one proof per
+    thread, Keccak constants hoisted. Each mode runs for about `seconds`; per-stage CPU ms per proof."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
     n = 1 << LOG_N
-    done, t0 = 0, time.perf_counter()
-    while True:
-        kw = synthetic.burn_inputs(10_000 + done)
-        st, air = O.air_from_inputs(kw["burn_amount"], kw["mint_amount"], kw["tx_prefix_hash"],
-                                    kw["recipient_address"], kw["secret"])
-        st, proof = O.prove(air, n, O.options(), faithful=True)
-        assert st == 0
-        done += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return {"value": done / el, "unit": "proofs/s", "cores": 1, "kind": "port",
-            "sample": f"{done} proofs (2^16 steps, blowup 8) by oracle/liboracle.so in {el:.1f}s, 1 thread, "
-                      "faithful per-row Keccak (src/burn_mint_air.rs:264,376)"}
+    opts = O.options()
+
+    def airs(base, k):
+        out = []
+        for i in range(k):
+            kw = synthetic.burn_inputs(base + i)
+            st, air = O.air_from_inputs(kw["burn_amount"], kw["mint_amount"], kw["tx_prefix_hash"],
+                                        kw["recipient_address"], kw["secret"])
+            assert st == 0
+            out.append(air)
+        return out
+
+    def run(faithful, threads, per_call):
+        done, used, stages, t0 = 0, 0, {}, time.perf_counter()
+        while True:
+            used, lens, sts, ms = O.prove_batch(airs(10_000 + done, per_call), n, opts, faithful, threads)
+            assert not any(sts), sts
+            done += per_call
+            for k, v in ms.items():
+                stages[k] = stages.get(k, 0.0) + v
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                return done, used, el, {k: round(v / done, 1) for k, v in stages.items()}
+
+    d1, _, el1, st1 = run(True, 1, 1)
+    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0))
+    d2, used2, el2, st2 = run(False, threads, threads)
+    return {"value": d1 / el1, "unit": "proofs/s", "cores": 1, "kind": "port",
+            "sample": f"{d1} proofs (2^16 steps, blowup 8) by oracle/liboracle.so in {el1:.1f}s, 1 thread, "
+                      "faithful per-row Keccak (src/burn_mint_air.rs:264,376)",
+            "stage_cpu_ms_per_proof": st1,
+            "all_cores": {"value": d2 / el2, "unit": "proofs/s", "cores": used2, "kind": "port",
+                          "sample": f"{d2} proofs by oracle/liboracle.so (OpenMP, {used2} threads, one proof "
+                                    f"per thread, Keccak constants hoisted) in {el2:.1f}s",
+                          "stage_cpu_ms_per_proof": st2},
+            "host": host_facts()}
+
+
+def verify_proofs(prover, proofs, inputs):
+    """every proof against the statement rebuilt from its inputs, on the GPU (xfg_verify_batch_gpu)
+    -> number accepted"""
+    import xfgstark
+    items = [(bytes(p), xfgstark.air_consts(**kw)) for p, kw in zip(proofs, inputs)]
+    return sum(xfgstark.XfgBurnMintVerifier().batch_verify(items, gpu=prover))
+
+
+def verify_rate(prover, proofs, inputs, threads=16, reps=3):
+    """side measurement, src/burn_mint_verifier.rs:326-408 batch verify: proofs/s of one batch through
+    the GPU batch verifier and through the host verifier on `threads` threads (best of `reps`)"""
+    import xfgstark
+    items = [(bytes(p), xfgstark.air_consts(**kw)) for p, kw in zip(proofs, inputs)]
+    v = xfgstark.XfgBurnMintVerifier()
+    best = {}
+    for name, kw in (("gpu", {"gpu": prover}), ("host", {"threads": threads})):
+        for _ in range(reps):
+            t = time.perf_counter()
+            ok = v.batch_verify(items, **kw)
+            dt = time.perf_counter() - t
+            assert all(ok)
+            best[name] = min(best.get(name, dt), dt)
+    return {"proofs": len(items), "gpu_proofs_per_s": round(len(items) / best["gpu"], 1),
+            "host_proofs_per_s": round(len(items) / best["host"], 1), "host_threads": threads}
 
 
 def main():
@@ -243,7 +344,10 @@ def main():
     ap.add_argument("--depth", type=int, default=6, help="batches in flight (pipelined submission)")
     ap.add_argument("--dist", action="store_true",
                     help="run the scatter / gather collectives even at world size 1 (exercises the RCCL "
-                         "path on a one-GPU box; launch with torch.distributed.run)")
+                         "path on a one-GPU box; launch with torch.distributed.run); rank 0 then also "
+                         "checks the gathered proofs byte for byte against a direct prove_batch")
+    ap.add_argument("--dump-proofs", default=None,
+                    help="rank 0 writes the last step's gathered proofs here (u32 LE length + bytes each)")
     args = ap.parse_args()
 
     import torch
@@ -308,12 +412,23 @@ def main():
     if dist is not None:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
     el = float(el_t.item())
+    pipe_ms, pipe_sets, pipe_polys = prover.lde_probe(False)
+    verified = None
     if rank == 0:
         assert out is not None and len(out) == per * world
+        last = [bytes(x) for x in out]
+        if args.dump_proofs:
+            with open(args.dump_proofs, "wb") as f:
+                for p in last:
+                    f.write(len(p).to_bytes(4, "little") + p)
+        # every proof of the last timed step (all ranks' shards, gathered in rank order) against the
+        # statement of the input it was scattered for: a sharding or ordering bug fails the run
+        verified = verify_proofs(prover, last, batches[-1])
+        if verified != len(last):
+            raise SystemExit(f"bench: {len(last) - verified} of {len(last)} proofs of the last step rejected")
         if args.dist:  # the collective path's output: the gathered proofs of the last step, in order
             want = [p.to_bytes() for p in prover.prove_batch(batches[-1], trace_length=n)]
-            assert [bytes(x) for x in out] == want, "gathered proofs differ from a direct prove_batch"
-    pipe_ms, pipe_sets, pipe_polys = prover.lde_probe(False)
+            assert last == want, "gathered proofs differ from a direct prove_batch"
 
     # one synchronous batch call (no pipelining), for reference
     t = time.perf_counter()
@@ -333,7 +448,8 @@ def main():
         prover.prove_batch([synthetic.burn_inputs(i) for i in range(per)], trace_length=n)
         prover_stage = {k: round(v, 3) for k, v in prover.stage_times().items()}
     prover.set_timing(False)
-    c5 = None if (args.no_config5 or rank != 0) else config5(prover)
+    vrate = verify_rate(prover, last[:per], batches[-1][:per]) if rank == 0 else None
+    c5 = None if (args.no_config5 or rank != 0) else config5(prover, gpu)
 
     if rank == 0:
         total = per * world * args.steps
@@ -368,6 +484,9 @@ def main():
                          # the same launch sets inside the timed pipelined steps (per XFG_UNIT-proof unit,
                          # sharing the GPU with the other lanes' kernels)
                          "in_pipeline": in_pipeline(pipe_ms, pipe_sets, pipe_polys, n)},
+            "whole_proof": whole_proof_line(total / el, n, world),
+            "verified": verified,
+            "verify": vrate,
             "stage_ms_one_batch": prover_stage,
             "sync_prove_batch_ms": round(sync_call_ms, 3),
         }

@@ -24,7 +24,7 @@
  * Output bytes are the proof's `StarkProof::to_bytes()` serialisation as restated in DESIGN.md
  * ("Proof format"); the caller owns all host buffers, the library owns device memory (pooled per
  * context). `out == NULL` (or *out_len too small) returns the required size in *out_len.
- * A context is bound to one HIP device; it owns XFG_LANES (default 5) lanes, each a HIP stream with
+ * A context is bound to one HIP device; it owns XFG_LANES (default 7) lanes, each a HIP stream with
  * its workspace and a host worker thread. Submit from one thread per context.
  */
 #ifndef XFG_STARK_H

@@ -88,6 +88,13 @@ void orc_build_trace(const orc_air* air, uint64_t n, uint64_t* trace);
  * proof bytes are identical either way. out == NULL -> *out_len = required size. */
 int orc_prove(const orc_air* air, const uint64_t* trace, uint64_t n, const orc_options* opt, int faithful,
               uint8_t* out, size_t* out_len, orc_debug* dbg);
+/* `count` proofs over `threads` OpenMP threads (bench.py's CPU baseline: 1 thread faithful, and all
+ * cores); stage_ms[ORC_NSTAGE] = summed CPU ms per stage: trace LDE, trace commitment, constraint
+ * evaluation, composition (+ commitment), OOD + DEEP, FRI, grinding + queries, serialisation.
+ * Returns the number of threads that ran. */
+#define ORC_NSTAGE 8
+int orc_prove_batch(const orc_air* airs, uint32_t count, uint64_t n, const orc_options* opt, int faithful,
+                    int threads, size_t* lens, int* statuses, double* stage_ms);
 /* evaluate_transition on one frame (src/burn_mint_air.rs:335-378) */
 void orc_eval_transition(const orc_air* air, const uint64_t cur[7], const uint64_t nxt[7], uint64_t r[7]);
 /* upper bound on proof size for buffer allocation */

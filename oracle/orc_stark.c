@@ -12,10 +12,32 @@
  * domain, Horner evaluation, naive 8-point interpolation for FRI folds) so that it shares no
  * structure with the HIP implementation it checks.
  */
+#define _POSIX_C_SOURCE 200809L
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 #include "oracle.h"
 #include "orc_prims.h"
+
+/* per-thread stage timers (orc_prove_batch): CPU milliseconds per prover stage, ORC_NSTAGE slots */
+static _Thread_local double* t_stage;
+static _Thread_local double t_mark;
+static double now_ms(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
+#define STAGE(i)                                   \
+    do {                                           \
+        if (t_stage) {                             \
+            const double t_ = now_ms();            \
+            t_stage[i] += t_ - t_mark;             \
+            t_mark = t_;                           \
+        }                                          \
+    } while (0)
 
 /* ============================================================ exported primitive wrappers */
 void orc_blake3_bytes(const uint8_t* in, size_t len, uint8_t out[32]) { orc_blake3(in, len, out); }
@@ -392,6 +414,7 @@ int orc_prove(const orc_air* air, const uint64_t* trace, uint64_t n, const orc_o
     const uint64_t beta = opt->blowup, N = n * beta, nce = CE_BLOWUP * n, f = opt->fri_folding;
     const uint64_t g = orc_root(ilog2u(n));
     int status = ORC_OK;
+    if (t_stage) t_mark = now_ms();
 
     /* Fiat-Shamir seed: Context::to_elements || pub_inputs.to_elements (ProverChannel::new) */
     uint64_t seed_e[20];
@@ -409,6 +432,7 @@ int orc_prove(const orc_air* air, const uint64_t* trace, uint64_t n, const orc_o
         orc_interpolate(coef + c * n, n, 1);
         orc_evaluate_lde(coef + c * n, n, beta, ORC_GEN, lde + c * N);
     }
+    STAGE(0);
     dg* leaves = (dg*)malloc(N * sizeof(dg));
     for (uint64_t k = 0; k < N; k++) {
         uint64_t row[W];
@@ -420,6 +444,7 @@ int orc_prove(const orc_air* air, const uint64_t* trace, uint64_t n, const orc_o
     bb_put(&commitments, ttree.nodes[1], 32);
     coin_reseed(&coin, ttree.nodes[1]);
     if (dbg) memcpy(dbg->trace_root, ttree.nodes[1], 32);
+    STAGE(1);
 
     /* 2. constraint composition coefficients: 7 transition + 8 boundary */
     uint64_t alpha[W], bcoef[NUM_ASSERT];
@@ -451,6 +476,7 @@ int orc_prove(const orc_air* air, const uint64_t* trace, uint64_t n, const orc_o
         acc = orc_add(acc, orc_mul(b1, orc_inv(orc_sub(x, g_last))));
         ce[i] = acc;
     }
+    STAGE(2);
 
     /* 4. composition polynomial: interpolate over the CE coset, keep num_cols*n = n coefficients
      * (num_constraint_composition_columns = 1 for degree-1 declarations -- RECALLED), LDE, commit */
@@ -465,6 +491,7 @@ int orc_prove(const orc_air* air, const uint64_t* trace, uint64_t n, const orc_o
     bb_put(&commitments, htree.nodes[1], 32);
     coin_reseed(&coin, htree.nodes[1]);
     if (dbg) memcpy(dbg->constraint_root, htree.nodes[1], 32);
+    STAGE(3);
 
     /* 5. OOD point, frame, DEEP coefficients */
     uint64_t z;
@@ -510,6 +537,7 @@ int orc_prove(const orc_air* air, const uint64_t* trace, uint64_t n, const orc_o
     uint64_t deg = 0;
     for (uint64_t j = 0; j < n; j++) if (t1[j]) deg = j;
     if (deg != n - 2) status = ORC_PROVER_ERROR; /* assert_eq!(trace_length - 2, degree) */
+    STAGE(4);
 
     /* 7. FRI layers (FriProver::build_layers) */
     uint32_t nl = num_fri_layers(N, opt);
@@ -550,6 +578,7 @@ int orc_prove(const orc_air* air, const uint64_t* trace, uint64_t n, const orc_o
     bb_put(&commitments, dtmp, 32);
     coin_reseed(&coin, dtmp);
     if (dbg) { memcpy(dbg->fri_roots[nl], dtmp, 32); dbg->num_fri_layers = nl; }
+    STAGE(5);
 
     /* 8. grinding + query positions (ProverChannel::grind_query_seed / get_query_positions) */
     uint64_t nonce = 1;
@@ -573,6 +602,7 @@ int orc_prove(const orc_air* air, const uint64_t* trace, uint64_t n, const orc_o
         dbg->num_unique_queries = (uint32_t)nu;
         for (uint64_t i = 0; i < nu; i++) dbg->positions[i] = pos[i];
     }
+    STAGE(6);
 
     /* 9. proof object + StarkProof::to_bytes (RECALLED layout, DESIGN.md §Proof format) */
     bbuf w = {0}, tmp = {0};
@@ -629,6 +659,7 @@ int orc_prove(const orc_air* air, const uint64_t* trace, uint64_t n, const orc_o
         else if (*out_len < w.n) { *out_len = w.n; status = ORC_BUFFER_TOO_SMALL; }
         else { memcpy(out, w.b, w.n); *out_len = w.n; }
     }
+    STAGE(7);
     free(w.b); free(tmp.b); free(commitments.b);
     for (uint32_t l = 0; l <= nl; l++) free(layer[l]);
     for (uint32_t l = 0; l < nl; l++) mtree_free(&ftree[l]);
@@ -636,6 +667,50 @@ int orc_prove(const orc_air* air, const uint64_t* trace, uint64_t n, const orc_o
     free(t1); free(t2); free(hcoef); free(hlde); free(ce); free(leaves); free(coef); free(lde);
     mtree_free(&ttree); mtree_free(&htree);
     return status;
+}
+
+/* CPU baseline driver (bench.py cpu_baseline): `count` independent proofs over `threads` OpenMP
+ * threads (0 = the OpenMP default), one proof per thread at a time -- the serial batch loop of the
+ * reference callers (src/benchmarks/mod.rs:301-342) spread over host cores. Proof bytes are
+ * discarded; lens / statuses per proof; stage_ms[ORC_NSTAGE] receives the CPU milliseconds per
+ * prover stage summed over all proofs (base-field proofs). Returns the threads that ran. */
+int orc_prove_batch(const orc_air* airs, uint32_t count, uint64_t n, const orc_options* opt, int faithful,
+                    int threads, size_t* lens, int* statuses, double* stage_ms) {
+    int used = 1;
+    for (int k = 0; k < ORC_NSTAGE; k++) stage_ms[k] = 0;
+#ifdef _OPENMP
+    if (threads <= 0) threads = omp_get_max_threads();
+#pragma omp parallel num_threads(threads)
+#endif
+    {
+        double mine[ORC_NSTAGE] = {0};
+        t_stage = mine;
+        const size_t cap = orc_proof_size_bound(n, opt);
+        uint8_t* buf = (uint8_t*)malloc(cap);
+        uint64_t* trace = (uint64_t*)malloc(7 * n * sizeof(uint64_t));
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+        for (int64_t i = 0; i < (int64_t)count; i++) {
+            orc_build_trace(&airs[i], n, trace);
+            size_t len = cap;
+            statuses[i] = orc_prove(&airs[i], trace, n, opt, faithful, buf, &len, NULL);
+            lens[i] = len;
+        }
+        free(trace);
+        free(buf);
+        t_stage = NULL;
+#ifdef _OPENMP
+#pragma omp critical
+#endif
+        {
+            for (int k = 0; k < ORC_NSTAGE; k++) stage_ms[k] += mine[k];
+#ifdef _OPENMP
+            used = omp_get_num_threads();
+#endif
+        }
+    }
+    return used;
 }
 
 /* ============================================================ verifier (self-check) */

@@ -59,6 +59,8 @@ def lib():
         L.orc_build_trace.argtypes = [C.POINTER(Air), C.c_uint64, u64p]
         L.orc_prove.argtypes = [C.POINTER(Air), u64p, C.c_uint64, C.POINTER(Options), C.c_int, u8p,
                                 C.POINTER(C.c_size_t), C.POINTER(Debug)]
+        L.orc_prove_batch.argtypes = [C.POINTER(Air), C.c_uint32, C.c_uint64, C.POINTER(Options), C.c_int, C.c_int,
+                                      C.POINTER(C.c_size_t), C.POINTER(C.c_int), C.POINTER(C.c_double)]
         L.orc_proof_size_bound.restype = C.c_size_t
         L.orc_proof_size_bound.argtypes = [C.c_uint64, C.POINTER(Options)]
         L.orc_verify.argtypes = [C.POINTER(Air), C.c_char_p, C.c_size_t, C.POINTER(Options)]
@@ -118,6 +120,22 @@ def prove(air, n, opts, trace=None, faithful=False, debug=False):
                          C.byref(dbg) if dbg is not None else None)
     proof = bytes(out[:ln.value]) if st == 0 else None
     return (st, proof, dbg) if debug else (st, proof)
+
+
+STAGES = ("trace_lde", "trace_commit", "constraint_eval", "composition", "ood_deep", "fri", "grinding_queries",
+          "serialize")
+
+
+def prove_batch(airs, n, opts, faithful=False, threads=0):
+    """orc_prove_batch: len(airs) proofs over `threads` OpenMP threads (0 = OpenMP default).
+    -> (threads used, [proof len], [status], {stage: summed CPU ms})"""
+    k = len(airs)
+    arr = (Air * k)(*airs)
+    lens = (C.c_size_t * k)()
+    sts = (C.c_int * k)()
+    ms = (C.c_double * len(STAGES))()
+    used = lib().orc_prove_batch(arr, k, n, C.byref(opts), 1 if faithful else 0, threads, lens, sts, ms)
+    return used, list(lens), list(sts), dict(zip(STAGES, ms))
 
 
 def verify(air, proof: bytes, opts) -> int:

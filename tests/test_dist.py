@@ -116,6 +116,55 @@ def torch_max(a, b):
     return torch.maximum(a, b.to(a.device))
 
 
+def _read_dump(path):
+    data, out, off = open(path, "rb").read(), [], 0
+    while off < len(data):
+        ln = int.from_bytes(data[off:off + 4], "little")
+        out.append(data[off + 4:off + 4 + ln])
+        off += 4 + ln
+    return out
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_real_prover(tmp_path):
+    """configs[3]'s sharded path with real proofs: bench.py under torch.distributed.run with TWO ranks
+    sharing the one GPU (XFG_DIST_BACKEND=gloo: host-side scatter / gather tensors; RCCL cannot run
+    two ranks on one device), 8 proofs per rank per step, 2^10-step traces. Rank 0 verifies every
+    gathered proof of the last step against its statement on the GPU and (--dist) checks them byte
+    for byte against a direct prove_batch of the same 16 inputs in order; here the dumped proofs are
+    checked against the oracle: two of them byte for byte, all 16 through the oracle verifier.
+    Started as a child process before this test process touches the GPU (the first GPU test of the
+    session). Reference batch pattern: src/burn_mint_verifier.rs:326-338."""
+    import json
+    import subprocess
+    import sys
+    import oracle_lib as O
+    import synthetic
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    dump = tmp_path / "proofs.bin"
+    per, world, steps, warmup, n = 8, 2, 2, 1, 1024
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", str(world), "--steps", str(steps), "--warmup", str(warmup), "--per-gpu", str(per),
+           "--log-n", "10", "--depth", "2", "--no-cpu-baseline", "--no-config5", "--dist",
+           "--dump-proofs", str(dump)]
+    env = dict(os.environ, XFG_DIST_BACKEND="gloo")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=root, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == world and line["verified"] == per * world
+    got = _read_dump(dump)
+    assert len(got) == per * world
+    last = [synthetic.burn_inputs((warmup + steps - 1) * per * world + i) for i in range(per * world)]
+    for i, kw in enumerate(last):
+        st, air = O.air_from_inputs(kw["burn_amount"], kw["mint_amount"], kw["tx_prefix_hash"],
+                                    kw["recipient_address"], kw["secret"])
+        assert st == 0 and O.verify(air, got[i], O.options()) == 0, i
+        if i in (0, per):  # the first proof of each rank's shard
+            st, want = O.prove(air, n, O.options())
+            assert st == 0 and got[i] == want, i
+
+
 @pytest.mark.gpu
 def test_gather_proofs_device_branch():
     import sys

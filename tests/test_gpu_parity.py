@@ -263,6 +263,35 @@ def test_submitted_batches_in_flight_match_oracle(prover):
             assert st == 0 and pr.to_bytes() == want
 
 
+def test_config2_full_batch_in_flight(prover):
+    """BASELINE configs[2] at its real size: two 64-proof batches of (n = 2^16, blowup 8, options
+    42/8/4/None/8/31) submitted together (depth 2, so both 32-proof units of each batch and the
+    lane splitting of the tail run as in bench.py). Proofs 0 and 63 equal the oracle's bytes, proof 0
+    (inputs syn0) equals the committed golden digest, and every one of the 128 proofs is accepted by
+    the GPU batch verifier, the host verifier and the oracle verifier (reference: every proof is what
+    prove_burn_mint returns, src/burn_mint_prover.rs:62-129; harness src/benchmarks/mod.rs:301-342)."""
+    import xfgstark
+    n = 1 << 16
+    prover._options = xfgstark.ProofOptions.reference()
+    batches = [[synthetic.burn_inputs(i) for i in range(64)], [synthetic.burn_inputs(64 + i) for i in range(64)]]
+    pend = [prover.submit_batch(kws, trace_length=n) for kws in batches]
+    res = [pb.result() for pb in pend]
+    proofs = [[p.to_bytes() for p in r] for r in res]
+    gold = [c for c in json.load(open(os.path.join(GOLD, "proofs.json"))) if c["name"] == "syn0_n65536_b8"][0]
+    assert len(proofs[0][0]) == gold["len"] and hashlib.sha256(proofs[0][0]).hexdigest() == gold["sha256"]
+    for i in (0, 63):
+        st, want = O.prove(oracle_air(batches[0][i]), n, O.options())
+        assert st == 0 and proofs[0][i] == want, i
+    v = xfgstark.XfgBurnMintVerifier()
+    for kws, ps in zip(batches, proofs):
+        items = [(p, xfgstark.air_consts(**kw)) for p, kw in zip(ps, kws)]
+        assert all(v.batch_verify(items, gpu=prover))
+        assert all(v.batch_verify(items))
+        for p, kw in zip(ps, kws):
+            assert O.verify(oracle_air(kw), p, O.options()) == 0
+    assert len(set(proofs[0] + proofs[1])) == 128
+
+
 def test_batch_isolates_invalid_inputs(prover):
     import xfgstark
     with_blowup(prover, 8)
@@ -427,6 +456,13 @@ def test_gpu_batch_verify_matches_host_verifier(prover, ext, n, blowup):
     dev = v.batch_verify(items, gpu=prover)
     assert dev == host
     assert sum(host) == len(proofs)  # exactly the untampered proofs with their own statement
+    # the oracle's own verifier on the same items: accepted exactly where the product accepts
+    oo = O.options(blowup=blowup, field_extension=ext)
+    for (p, a), ok in zip(items, host):
+        oa = O.Air()
+        oa.pub = (O.C.c_uint64 * 12)(*a[0])
+        oa.nullifier, oa.commitment = a[1], a[2]
+        assert (O.verify(oa, p, oo) == 0) == ok
     other = xfgstark.ProofOptions.reference()
     other.num_queries = 41
     assert not any(xfgstark.XfgBurnMintVerifier(proof_options=other).batch_verify(items[:3], gpu=prover))
@@ -445,3 +481,15 @@ def test_rejects_options_the_reference_rejects(prover):
     with_blowup(prover, 8)
     with pytest.raises(xfgstark.XfgStarkError):
         prover.prove_burn_mint(**kw, trace_length=100)
+
+
+def test_submit_rejects_empty_and_unsized_batches(prover):
+    """an empty batch and a trace length with no proof-size bound reach the C library, which reports
+    XFG_INVALID_ARGUMENT / PROVER_ERROR as XfgStarkError (not a bare ValueError from the buffer pool)"""
+    import xfgstark
+    prover._options = xfgstark.ProofOptions.reference()
+    prover.__dict__.get("_free", []).clear()
+    with pytest.raises(xfgstark.XfgStarkError):
+        prover.submit_batch([], trace_length=1024).result()
+    with pytest.raises(xfgstark.XfgStarkError):
+        prover.submit_batch([synthetic.burn_inputs(1)], trace_length=100).result()

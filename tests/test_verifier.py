@@ -165,14 +165,29 @@ def test_noncanonical_elements_rejected(X):
         bad = _set_elem(proof, at, 0xFFFFFFFFFFFFFFFF)
         ok, err, _ = v.verify_with_details(bad, air)
         assert not ok and err == 'ProofDeserializationError("invalid field element")', (name, err)
-        with pytest.raises(X.XfgStarkError):
-            X.StarkProof.from_bytes(bad)
+        # Proof::from_bytes keeps the element sections as raw bytes (winterfell 0.8): structural only
+        assert X.StarkProof.from_bytes(bad).to_bytes() == bad
     # p itself is non-canonical too; p - 1 parses (and then fails a check, not the parser)
     at = sec["remainder"][0]
     ok, err, _ = v.verify_with_details(_set_elem(proof, at, P), air)
     assert not ok and err.startswith("ProofDeserializationError"), err
     ok, err, _ = v.verify_with_details(_set_elem(proof, at, P - 1), air)
     assert not ok and err.startswith("FriVerificationFailed"), err
+
+
+def test_options_checked_before_elements(X):
+    """error precedence of winterfell::verify: the acceptable-options check comes before
+    VerifierChannel::new deserialises the element sections (ADVICE r02), so a proof with other
+    options AND a value >= p reports UnacceptableProofOptions"""
+    kws = synthetic.burn_inputs(5)
+    proof = _oracle_proof(kws, 256)
+    bad = _set_elem(proof, _sections(proof)["remainder"][0], 0xFFFFFFFFFFFFFFFF)
+    other = X.ProofOptions.reference()
+    other.num_queries = 41
+    ok, err, _ = X.XfgBurnMintVerifier(proof_options=other).verify_with_details(bad, _statement(X, kws))
+    assert not ok and err == "UnacceptableProofOptions", err
+    ok, err, _ = X.XfgBurnMintVerifier().verify_with_details(bad, _statement(X, kws))
+    assert not ok and err == 'ProofDeserializationError("invalid field element")', err
 
 
 def test_from_bytes_remainder_len_counts_elements(X):

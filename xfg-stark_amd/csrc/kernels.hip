@@ -150,6 +150,8 @@ __device__ void coin_root_step(const CoinStep& cs, int b, const Digest& root) {
         } else if (lane == 0) {  // FRI layer alpha, stored as alpha * 7^-1 for the fold
             const u64 inv7 = 0x249249246DB6DB6EULL;
             for (int k = 0; k < D; k++) cs.out[(u64)b * D + k] = gl_mul(a[k], inv7);
+            if (cs.hist)
+                for (int k = 0; k < D; k++) cs.hist[(u64)b * D + k] = a[k];
         }
     }
     if (lane == 0) {
@@ -570,9 +572,11 @@ __global__ __launch_bounds__(256) void ood_kernel(const u64* coef, const u64* hc
         acc[14] = fe_add(acc[14], fe_mul(hc, pz));
         pz = fe_mul(pz, zT);
         pzg = fe_mul(pzg, zgT);
+        if (r + 1 < OOD_R) {  // (the last iteration loaded nothing)
 #pragma unroll
-        for (int c = 0; c < 7; c++) cur[c] = nxt[c];
-        hc = hn;
+            for (int c = 0; c < 7; c++) cur[c] = nxt[c];
+            hc = hn;
+        }
     }
     // wave reduction, then across the (up to 4) waves
     const int W = T < 64 ? T : 64;

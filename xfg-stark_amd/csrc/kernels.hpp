@@ -86,6 +86,7 @@ struct CoinStep {
     u64* out = nullptr;
     u64 g = 0;                  // OOD_POINT: the trace domain generator
     Digest* root_out = nullptr;  // root of proof b also stored at root_out[b] (one contiguous D2H)
+    u64* hist = nullptr;         // FRI_ALPHA: the raw alpha of proof b also stored at hist[b][D]
 };
 // step run by launch_ood on the OOD frame (when coins is set): reseed with hash(trace frame) and
 // hash(H(z)), draw a_0..a_6 and gamma, and form the DEEP parameters dp [B] from zpts [B][2][D]

@@ -274,7 +274,7 @@ struct Lane {
     u64 lde_sets = 0, lde_polys = 0;
     DBuf<AirConst> air;
     DBuf<u64> coeffs, trace, coef, scratch, lde, ce, hcoef, hlde, zpts, partial, ood, carry, deep, f0, alpha7,
-        rem, gidx, gval, dn2;
+        rem, gidx, gval, dn2, falpha;
     DBuf<Digest> tnodes, hnodes, gdig, droots;
     DBuf<DeepParams> dp;
     DBuf<DevCoin> dcoin;  // device-side transcript
@@ -283,7 +283,7 @@ struct Lane {
     std::vector<DBuf<Digest>> fnodes;
     // pinned host staging
     HBuf<Digest> h_roots, h_gd;
-    HBuf<u64> h_co, h_ood, h_rem, h_dn2, h_idx, h_gv;
+    HBuf<u64> h_co, h_ood, h_rem, h_dn2, h_idx, h_gv, h_falpha;
     HBuf<AirConst> h_air;
     HBuf<DevCoin> h_coin;
     HBuf<DeepParams> h_dp;
@@ -297,7 +297,7 @@ struct Lane {
     } hs;
     void release() {
         for (auto* b : {&h_roots, &h_gd}) b->release();
-        for (auto* b : {&h_co, &h_ood, &h_rem, &h_dn2, &h_idx, &h_gv}) b->release();
+        for (auto* b : {&h_co, &h_ood, &h_rem, &h_dn2, &h_idx, &h_gv, &h_falpha}) b->release();
         h_air.release();
         h_coin.release();
         h_dp.release();
@@ -306,7 +306,7 @@ struct Lane {
         dfail.release();
         air.release();
         for (auto* b : {&coeffs, &trace, &coef, &scratch, &lde, &ce, &hcoef, &hlde, &zpts, &partial, &ood,
-                        &carry, &deep, &f0, &alpha7, &rem, &gidx, &gval, &dn2})
+                        &carry, &deep, &f0, &alpha7, &rem, &gidx, &gval, &dn2, &falpha})
             b->release();
         for (auto* b : {&tnodes, &hnodes, &gdig, &droots}) b->release();
         dp.release();
@@ -523,6 +523,7 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     c->deep.ensure((size_t)B * DE * n);
     c->f0.ensure((size_t)B * DE * N);
     c->alpha7.ensure((size_t)B * DE);
+    c->falpha.ensure((size_t)std::max(1u, nl) * B * DE);
     c->dn2.ensure((size_t)B * DE);
     if (c->flayer.size() < nl + 1) {
         c->flayer.resize(nl + 1);
@@ -652,6 +653,7 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
                                     s);
         cs.kind = CoinStep::FRI_ALPHA;
         cs.out = c->alpha7.p;
+        cs.hist = c->falpha.p + (size_t)l * B * DE;  // the raw alpha of this layer, for the replay
         cs.root_out = c->droots.p + (size_t)(2 + l) * B;
         launch_tree_top(c->fnodes[l].p, 2 * rows, top, B, s, cs);
         launch_fri_fold(src, sstride, cstride, cm, logn, logbeta, rows, (int)ilog2(D[l]), c->alpha7.p,
@@ -668,6 +670,8 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     DeepParams* dps = c->h_dp.ensure(B);
     HIPCHK(hipMemcpyAsync(dps, c->dp.p, B * sizeof(DeepParams), hipMemcpyDeviceToHost, s));
     const Digest* froots = roots + 2 * B;
+    u64* falpha = c->h_falpha.ensure((size_t)std::max(1u, nl) * B * DE);  // [layer][B][DE]
+    if (nl) HIPCHK(hipMemcpyAsync(falpha, c->falpha.p, (size_t)nl * B * DE * 8, hipMemcpyDeviceToHost, s));
     int* ffail = c->h_fail.ensure(B);
     HIPCHK(hipMemcpyAsync(ffail, c->dfail.p, B * sizeof(int), hipMemcpyDeviceToHost, s));
     // remainder: interpolate the last layer over 7*<w_D>, keep D/blowup coefficients
@@ -716,7 +720,21 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         draw(P.gamma);
         for (unsigned l = 0; l < nl; l++) {
             commit(froots[(size_t)l * B + b]);
-            draw(nullptr);  // FRI alpha
+            draw(falpha + ((size_t)l * B + b) * DE);  // FRI alpha (the fold used alpha * 7^-1 of it)
+        }
+        // the DEEP parameters the device derived from z and the frame: z g, 1 / z, 1 / (z g), and the
+        // OOD sums c1 = gamma H(z) + sum a_k T_k(z), c2 = sum a_k T_k(z g)
+        if (!failed) {
+            auto e = [&](const u64* v) { return E2{v[0], DE == 2 ? v[1] : 0}; };
+            auto ood_e = [&](int q) { return E2{j.ood[q * DE], DE == 2 ? j.ood[q * DE + 1] : 0}; };
+            const E2 z = e(P.z), zg = e(P.zg), one = e2(1);
+            E2 c1 = e2_mul(e(P.gamma), ood_e(14)), c2{0, 0};
+            for (int k = 0; k < 7; k++) {
+                c1 = e2_add(c1, e2_mul(e(P.a[k]), ood_e(2 * k)));
+                c2 = e2_add(c2, e2_mul(e(P.a[k]), ood_e(2 * k + 1)));
+            }
+            same &= e2_eq(zg, e2_mulb(z, cs.g)) && e2_eq(e2_mul(z, e(P.zinv)), one) &&
+                    e2_eq(e2_mul(zg, e(P.zginv)), one) && e2_eq(c1, e(P.c1)) && e2_eq(c2, e(P.c2));
         }
         if (failed) j.status = XFG_PROVER_ERROR;
         if (failed != (ffail[b] != 0) || !same) throw std::runtime_error("device / host transcript diverged");
@@ -862,9 +880,13 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     {
         // the segments lie end to end in allidx: values first, then digests
         GatherSet gs;
-        size_t vo = 0, dof = 0;
+        size_t vo = 0, dof = 0, gbase = 0;  // gbase: index entries consumed by launches already made
         auto add = [&](const void* src, void* dst, bool dig, size_t cnt) {
-            if (gs.nseg == GatherSet::MAX) throw std::runtime_error("too many FRI layers for one gather launch");
+            if (gs.nseg == GatherSet::MAX) {  // very deep FRI: flush and continue in a new launch
+                launch_gather_set(gs, c->gidx.p + gbase, s);
+                gbase += gs.first[gs.nseg];
+                gs = GatherSet{};
+            }
             gs.src[gs.nseg] = src;
             gs.dst[gs.nseg] = dst;
             gs.digest[gs.nseg] = dig ? 1 : 0;
@@ -882,7 +904,7 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
             add(src, c->gdig.p + dof, true, dseg[k].second);
             dof += dseg[k].second;
         }
-        launch_gather_set(gs, c->gidx.p, s);
+        launch_gather_set(gs, c->gidx.p + gbase, s);
         const u64* ent = c->gidx.p + nvals + ndig;
         launch_open_rows(c->lde.p, 7, ent, nent, c->gdig.p + ndig, logn, logbeta, s);
         launch_open_rows(c->hlde.p, DE, ent, nent, c->gdig.p + ndig + nopen, logn, logbeta, s);
@@ -1390,7 +1412,7 @@ int xfg_prove_batch_submit(xfg_ctx* c, uint32_t count, const xfg_burn_inputs* in
     if (!c) return XFG_INVALID_ARGUMENT;
     c->err.clear();
     if (!inputs || !opts || !out_lens || !statuses || !ticket || count == 0) {
-        c->err = "null argument";
+        c->err = count == 0 ? "empty batch" : "null argument";
         return XFG_INVALID_ARGUMENT;
     }
     *ticket = 0;

@@ -60,9 +60,11 @@ static bool read_span(Reader& r, int len_bytes, Span& s) {
     s.p = r.take(s.n);
     return !r.bad;
 }
-// every field element of a proof is canonical: winter-math 0.8 BaseElement::read_from rejects a
-// value >= p, so a non-canonical encoding fails deserialization here too (and the field code on
-// both the host and the GPU verifier may then assume canonical operands)
+// every field element of a proof must be canonical: winter-math 0.8 BaseElement::read_from rejects
+// a value >= p. Winterfell reads the element sections (queries, OOD frame, FRI layers, remainder)
+// only in VerifierChannel::new, after the acceptable-options check, so parse_proof (from_bytes)
+// stays structural and verify_transcript runs this check after the options (the field code of
+// the host and GPU verifiers then assumes canonical operands)
 static bool canonical_elems(const Span& s) {
     if (s.n % 8) return false;
     for (size_t i = 0; i < s.n / 8; i++)
@@ -96,7 +98,7 @@ std::string parse_proof(const uint8_t* bytes, size_t len, ParsedProof& pf) {
     const uint8_t* c = r.take(clen);
     if (!c || clen % 32) return "ProofDeserializationError(\"commitments\")";
     pf.com.resize(clen / 32);
-    memcpy(pf.com.data(), c, clen);
+    if (clen) memcpy(pf.com.data(), c, clen);  // (an empty vector's data() may be null)
     if (r.u(1) != 1) return "ProofDeserializationError(\"trace queries: expected one segment\")";
     if (!read_span(r, 4, pf.trace_rows)) return "ProofDeserializationError(\"trace queries\")";
     const u64 tpl = r.u(4);
@@ -115,20 +117,15 @@ std::string parse_proof(const uint8_t* bytes, size_t len, ParsedProof& pf) {
     pf.ood.p += 1;
     pf.ood.n -= 1;
     pf.hz = hz;
-    if (!canonical_elems(pf.trace_rows) || !canonical_elems(pf.constraint_rows) || !canonical_elems(pf.ood) ||
-        !canonical_elems(pf.hz))
-        return "ProofDeserializationError(\"invalid field element\")";
     const u64 nl = r.u(1);
     pf.fri_vals.resize(nl);
     pf.fri_paths.resize(nl);
     for (u64 l = 0; l < nl; l++) {
         if (!read_span(r, 4, pf.fri_vals[l])) return "ProofDeserializationError(\"FRI layer values\")";
-        if (!canonical_elems(pf.fri_vals[l])) return "ProofDeserializationError(\"invalid field element\")";
         const u64 pl = r.u(4);
         if (r.bad || !read_paths(r, pl, pf.fri_paths[l])) return "ProofDeserializationError(\"FRI layer paths\")";
     }
     if (!read_span(r, 2, pf.fri_rem) || pf.fri_rem.n % esz) return "ProofDeserializationError(\"FRI remainder\")";
-    if (!canonical_elems(pf.fri_rem)) return "ProofDeserializationError(\"invalid field element\")";
     pf.partitions = r.u(1);
     pf.nonce = r.u(8);
     if (r.bad) return "ProofDeserializationError(\"unexpected end of input\")";
@@ -274,6 +271,11 @@ std::string verify_transcript(const uint8_t* bytes, size_t len, const AirConst& 
     if (memcmp(&o, &acceptable, sizeof o)) return "UnacceptableProofOptions";  // AcceptableOptions::OptionSet
     const u64 n = 1ULL << pf.logn;
     if (check_options(n, o)) return "UnacceptableProofOptions";
+    // VerifierChannel::new: the element sections are deserialised now
+    bool canon = canonical_elems(pf.trace_rows) && canonical_elems(pf.constraint_rows) && canonical_elems(pf.ood) &&
+                 canonical_elems(pf.hz) && canonical_elems(pf.fri_rem);
+    for (const Span& v : pf.fri_vals) canon = canon && canonical_elems(v);
+    if (!canon) return "ProofDeserializationError(\"invalid field element\")";
     const int de = (int)o.ext;  // E = base field (1) or its quadratic extension (2)
     const u64 beta = o.beta, N = n * beta;
     const unsigned nl = num_fri_layers(N, o);

@@ -483,6 +483,9 @@ class XfgBurnMintProver:
         for i, b in enumerate(free):
             if C.sizeof(b) >= size:
                 return free.pop(i)
+        # at least one byte: an anonymous mapping of length 0 raises ValueError before the C library
+        # could report the invalid request (empty batch, trace length with no size bound)
+        size = max(size, 1)
         return (C.c_char * size).from_buffer(_anon_map(size))
 
     def prepare(self, count, trace_length=64, buffers=0):
