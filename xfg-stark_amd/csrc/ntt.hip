@@ -201,6 +201,9 @@ struct NttArgs {
     const u64* pt;  // pass tables: w_R^(+-i) [R], w_C^(+-i) [C], forward coset pre-factors [beta][R]; or nullptr
     int xcd;        // 1: XCD-contiguous block order (see xcd_block)
     int tq_b;       // forward: pass B applies the four-step twiddles as it loads (ntt_pass_a_cos)
+    int preg;       // forward pass A: coset pre-factors read from the pass tables in L2, not LDS
+    int yblk;       // forward, no four-step table: the intermediate is stored in column blocks of
+                    // 2^yblk columns ([j2 >> yblk][k1][j2 & mask]) instead of rows [k1][j2]
     Tables T;
 };
 
@@ -250,7 +253,7 @@ __global__ __launch_bounds__(1 << LOGT, (1 << (10 - LOGT)) >> (LOGE - 4)) void n
         // contiguous per-size tables (behind the four-step table, or standalone): coalesced loads
         for (int i = threadIdx.x; i < R; i += NT) {
             ltw[i] = a.pt[i];
-            if (!INV) pre[i] = a.pt[R + (1 << a.logC) + t * R + i];
+            if (!INV && !a.preg) pre[i] = a.pt[R + (1 << a.logC) + t * R + i];
         }
     } else {
         for (int i = threadIdx.x; i < R; i += NT) {
@@ -264,9 +267,11 @@ __global__ __launch_bounds__(1 << LOGT, (1 << (10 - LOGT)) >> (LOGE - 4)) void n
     const u64* in = a.in + (u64)poly * a.in_stride;
     u64* y = a.y + (u64)pt * n;
     const auto rin = buf_rsrc(in + col0), ry = buf_rsrc(y + col0);
+    const u64* preg = (!INV && a.preg) ? a.pt + R + (1 << a.logC) + (u64)t * R : nullptr;
     auto ldg = [&](int seq, int j, int o) -> u64 {
         const u64 v = buf_ld(rin, (((u32)j << a.logC) + seq) * 8, ((u32)o << a.logC) * 8);
-        return INV ? v : gl_mul(v, pre[j + o]);
+        if (INV) return v;
+        return gl_mul(v, preg ? preg[j + o] : pre[j + o]);
     };
     // four-step twiddles from the table: loaded by pf before the last step's loads and butterflies,
     // so the table latency hides behind them; one multiply per element instead of two
@@ -305,9 +310,14 @@ __global__ __launch_bounds__(1 << LOGT, (1 << (10 - LOGT)) >> (LOGE - 4)) void n
         }
         u64 w = INV ? wq[q] : gl_mul(p7q[q], wq[q]);
         const u64 step = sq[q];
+        // blocked intermediate: this column's block, rows of 2^yblk words (whole lines per store
+        // instruction however narrow the tile)
+        const int B = a.yblk;
+        const u64 cb = B ? ((j2 >> B) << (a.logR + B)) + (j2 & ((1u << B) - 1)) : j2;
+        const int rs = B ? B : a.logC;
 #pragma unroll
         for (int r = 0; r < RR; r++) {
-            y[((u64)(base + r * stride) << a.logC) + j2] = gl_mul(v[r], w);
+            y[((u64)(base + r * stride) << rs) + cb] = gl_mul(v[r], w);
             if (r + 1 < RR) w = gl_mul(w, step);
         }
     };
@@ -417,6 +427,11 @@ __global__ __launch_bounds__(1 << LOGT) void ntt_pass_b(NttArgs a) {
             if (tqb) return gl_mul(yv[o / G1], tv[o / G1]);
         }
         const u64 i = ((u64)(k10 + seq) << LOGC) + j + o;
+        if (!INV && a.yblk) {  // blocked intermediate (pass A stored column blocks)
+            const int B = a.yblk;
+            const u64 j2 = (u64)(j + o);
+            return y[((j2 >> B) << (a.logR + B)) + ((u64)(k10 + seq) << B) + (j2 & ((1u << B) - 1))];
+        }
         return tqb ? gl_mul(y[i], tqb[i]) : y[i];
     };
     const auto rout = buf_rsrc(a.out + (u64)pt * n + k10);
@@ -440,6 +455,60 @@ __global__ __launch_bounds__(1 << LOGT) void ntt_pass_b(NttArgs a) {
     // sequences so the (final) global store is coalesced
     pass_dft<LOGC, LOGE, INV, (Plan<LOGC, LOGE>::NSTEP == 1), NT>(tile, logTR, ltw, ldg, stg,
                                                                    [](int, int, int, int) {});
+}
+
+// ---------------------------------------------------------------- pass B, persistent (forward, no table)
+// The row DFTs of an LDE past the four-step tables (configs[4]: 2^24 points, radix 32 x 32, 8 rows
+// per tile, two blocks per CU). One tile per block waited on its loads for 48 % of its wave cycles
+// (profiles/r02/lde_pmc_2p16_vs_2p20.json): here a block loops over its share of the (row tile,
+// poly-coset) tiles and issues the next tile's first-step loads into registers before it
+// transforms the current one, so one tile's loads are in flight during the other's butterflies.
+// Tiles are dealt per XCD in contiguous ranges (the blocks of XCD x = blockIdx % 8 walk the x-th
+// eighth of the tiles side by side), so the 64-byte output runs of neighbouring tiles meet in
+// one L2, as xcd_block arranges for the one-tile form.
+template <int LOGC, int LOGT, int LOGE>
+__global__ __launch_bounds__(1 << LOGT, 2) void ntt_pass_b_pers(NttArgs a, int ntx, int ntiles) {
+    constexpr int C = 1 << LOGC, RR = Plan<LOGC, LOGE>::LAST_R, NT = 1 << LOGT;
+    using PLB = Plan<LOGC, LOGE>;
+    constexpr int R1 = 1 << PLB::FIRST_LOGR, G1 = C / R1;
+    static_assert(PLB::NSTEP > 1 && (1 << LOGE) == R1, "one full-radix first-step group per thread");
+    constexpr int logTR = LOGT + LOGE - LOGC, TR = 1 << logTR;
+    extern __shared__ u64 lds[];
+    u64* tile = lds;
+    u64* ltw = lds + TR * row_pitch(C, LOGE, logTR);
+    {
+        const u64* pt4 = a.pt + (1 << a.logR);
+        for (int i = threadIdx.x; i < C; i += NT) ltw[i] = pt4[i];
+    }
+    __syncthreads();
+    const u64 n = 1ULL << a.logn;
+    const int per_x = gridDim.x >> 3, x = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    const int span = (ntiles + 7) >> 3, tend = min((x + 1) * span, ntiles);
+    const int seq0 = threadIdx.x / G1, j0 = threadIdx.x % G1;
+    auto load = [&](int ti, u64* dst) {
+        const int pt = ti / ntx, k10 = (ti - pt * ntx) * TR;
+        const u64* y = a.y + (u64)pt * n + ((u64)(k10 + seq0) << LOGC) + j0;
+#pragma unroll
+        for (int r = 0; r < R1; r++) dst[r] = y[r * G1];
+    };
+    int ti = x * span + slot;
+    u64 yv[R1];
+    if (ti < tend) load(ti, yv);
+    for (; ti < tend; ti += per_x) {
+        const int pt = ti / ntx, k10 = (ti - pt * ntx) * TR;
+        u64 nx[R1];
+        if (ti + per_x < tend) load(ti + per_x, nx);
+        auto ldg = [&](int, int, int o) -> u64 { return yv[o / G1]; };
+        const auto rout = buf_rsrc(a.out + (u64)pt * n + k10);
+        auto stg = [&](int, int seq, int base, int stride, u64* v) {
+#pragma unroll
+            for (int r = 0; r < RR; r++)
+                buf_st(rout, (seq + ((u32)base << a.logR)) * 8, ((u32)(r * stride) << a.logR) * 8, canon(v[r]));
+        };
+        pass_dft<LOGC, LOGE, false, false, NT>(tile, logTR, ltw, ldg, stg, [](int, int, int, int) {});
+#pragma unroll
+        for (int r = 0; r < R1; r++) yv[r] = nx[r];
+    }
 }
 
 // ---------------------------------------------------------------- dispatch
@@ -652,8 +721,17 @@ static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
         const char* v = getenv("XFG_NTT_E");
         return !(v && *v == '4');
     }();
-    const int eA = (e5_on && wide_on && a.logR >= 9 && a.logR <= 10 && a.logC >= 4) ? 5 : 4;
-    const int eB = (e5_on && wide_on && a.logC >= 9 && a.logC <= 10 && a.logR >= 3) ? 5 : 4;
+    // XFG_NTT_EA=4 / XFG_NTT_EB=4: radix-16 in pass A / pass B only (A/B knobs)
+    static const bool e5a = [] {
+        const char* v = getenv("XFG_NTT_EA");
+        return !(v && *v == '4');
+    }();
+    static const bool e5b = [] {
+        const char* v = getenv("XFG_NTT_EB");
+        return !(v && *v == '4');
+    }();
+    const int eA = (e5_on && e5a && wide_on && a.logR >= 9 && a.logR <= 10 && a.logC >= 4) ? 5 : 4;
+    const int eB = (e5_on && e5b && wide_on && a.logC >= 9 && a.logC <= 10 && a.logR >= 3) ? 5 : 4;
     const bool capA = a.logR >= 9 && a.logR <= 10 && a.logC >= 4, capB = a.logC >= 9 && a.logC <= 11 && a.logR >= 4;
     int ltA = capA ? (force_lta >= 8 && force_lta <= 10 ? force_lta : (wide_on ? 10 : 8)) : 8;
     // pass B: 512 threads (8192 elements, <= 78 KiB, two blocks per CU) up to C = 1024 -- the second
@@ -661,12 +739,23 @@ static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
     int ltB = capB ? (force_ltb >= 8 && force_ltb <= 10 ? force_ltb : (wide_on ? (a.logC <= 10 ? 9 : 10) : 8)) : 8;
     // radix-32 tiles: pass A 16 columns (512 threads at R = 1024, 256 at R = 512), pass B 8192
     // elements (256 threads, two blocks per CU); forced thread counts limited to 256 / 512
-    if (eA == 5) ltA = (force_lta == 8 || force_lta == 9) ? force_lta : a.logR - 1;
+    // (forward R = 1024, configs[4]: 256 threads x 8 columns with the coset pre-factors read from L2
+    // -- 76 KiB of LDS, two blocks per CU -- pass A 828 -> 790 us per 2^24-point trace LDE, same box)
+    if (eA == 5) ltA = (force_lta == 8 || force_lta == 9) ? force_lta : (!inv && a.logR == 10 && a.pt ? 8 : a.logR - 1);
     if (eB == 5) ltB = (force_ltb == 8 || force_ltb == 9) ? force_ltb : 8;
     const int logTC = a.logC < ltA + eA - a.logR ? a.logC : ltA + eA - a.logR;
     const int logTR = a.logR < ltB + eB - a.logC ? a.logR : ltB + eB - a.logC;
     const int ncos = inv ? 1 : (1 << a.logbeta);
-    size_t lds_a = ((size_t)(1 << logTC) * row_pitch(R, eA, ltA + eA - a.logR) + 2 * R) * sizeof(u64);
+    // forward pass A of radix-32 tiles reads its coset pre-factors from the pass tables (L2) instead
+    // of an LDS copy: R words less LDS per block (XFG_NTT_PREG=0 / 1 forces it off / on elsewhere)
+    static const int preg_env = [] {
+        const char* v = getenv("XFG_NTT_PREG");
+        return v && *v ? atoi(v) : -1;
+    }();
+    const bool preg_dflt = eA == 5 && ltA == 8 && a.logR == 10;
+    a.preg = (!inv && a.pt && !(a.t4 && a.logR == 8 && ltA == 8 && eA == 4) &&  // (not the cos kernel)
+              (preg_env < 0 ? preg_dflt : preg_env == 1)) ? 1 : 0;
+    size_t lds_a = ((size_t)(1 << logTC) * row_pitch(R, eA, ltA + eA - a.logR) + (a.preg ? 1 : 2) * R) * sizeof(u64);
     size_t lds_b = ((size_t)(1 << logTR) * row_pitch(C, eB, ltB + eB - a.logC) + C) * sizeof(u64);
     dim3 ga(C >> logTC, npoly * ncos), gb(R >> logTR, npoly * ncos);
     // tile rows narrower than 16 words (a 128 B line) in the scattered writes: pass A stores TC
@@ -675,7 +764,14 @@ static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
         const char* v = getenv("XFG_NTT_XCD");
         return !(v && *v == '0');
     }();
-    a.xcd = xcd_on ? ((logTC < 4 ? 1 : 0) | (logTR < 4 ? 2 : 0)) : 0;
+    // XFG_NTT_YBLK=1: forward LDE without a four-step table stores the intermediate in column blocks
+    // of the pass-A tile width (A/B knob)
+    static const bool yblk_on = [] {
+        const char* v = getenv("XFG_NTT_YBLK");
+        return v && *v == '1';
+    }();
+    a.yblk = (!inv && !a.t4 && yblk_on) ? logTC : 0;
+    a.xcd = xcd_on ? ((logTC < 4 && !a.yblk ? 1 : 0) | (logTR < 4 ? 2 : 0)) : 0;
     if (inv) {
         run_pass_a<true>(a.logR, ltA, eA, ga, lds_a, s, a);
         run_pass_b<true>(a.logC, ltB, eB, gb, lds_b, s, a);
@@ -690,7 +786,19 @@ static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
             hipLaunchKernelGGL(ntt_pass_a_cos<8>, dim3(C >> logTC, npoly), dim3(256), lds_a, s, a);
         } else
             run_pass_a<false>(a.logR, ltA, eA, ga, lds_a, s, a);
-        run_pass_b<false>(a.logC, ltB, eB, gb, lds_b, s, a);
+        // persistent pass B past the four-step tables (XFG_NTT_BPERS=0 disables, for A/B runs)
+        static const bool bpers_on = [] {
+            const char* v = getenv("XFG_NTT_BPERS");
+            return !(v && *v == '0');
+        }();
+        if (bpers_on && eB == 5 && ltB == 8 && a.logC == 10 && a.logR >= 3 && !a.t4 && a.pt && !a.yblk) {
+            const int ntx = R >> logTR, ntiles = ntx * npoly * ncos;
+            int dev = 0, cus = 256;
+            if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            const int nb = std::max(8, std::min(2 * cus, ntiles) & ~7);
+            hipLaunchKernelGGL((ntt_pass_b_pers<10, 8, 5>), dim3(nb), dim3(256), lds_b, s, a, ntx, ntiles);
+        } else
+            run_pass_b<false>(a.logC, ltB, eB, gb, lds_b, s, a);
     }
 }
 
