@@ -75,41 +75,73 @@ def scatter_inputs(all_inputs, rank, world, per_rank, device, dist, packed=None)
     return unpack_inputs(local.cpu().numpy())
 
 
+class _Exchange:
+    """reused buffers of gather_proofs: a pinned host record per rank (double-buffered, so a record
+    is never rewritten while its host-to-device copy may still run), rank 0's device gather buffer
+    and its pinned host copy"""
+    send = None
+    flip = 0
+    big = None
+    host = None
+
+
+def _pinned(nbytes, device):
+    import torch
+    return torch.empty(nbytes, dtype=torch.uint8, pin_memory=device.type == "cuda")
+
+
 def gather_proofs(proofs, rank, world, per_rank, device, dist):
-    """this rank's proof bytes -> all proofs on rank 0 (None elsewhere) over the process group: one
-    gather of [per_rank int64 lengths | concatenated proofs], padded to the longest rank payload;
-    rank 0 gets zero-copy memoryviews into the gathered buffer (one D2H for all ranks into a reused
-    pinned buffer: the views stay valid until the next call)"""
+    """this rank's proofs -> all proofs on rank 0 (None elsewhere) over the process group: one gather
+    of [per_rank int64 lengths | concatenated proofs], padded to the longest rank record.
+    `proofs` is a list of proof bytes or a submitted batch (xfgstark.PendingBatch), whose proofs
+    are packed straight from the workers' output buffer into a pinned record. Rank 0 gathers into
+    one reused device buffer, copies it to pinned host memory in one D2H and returns zero-copy
+    memoryviews into it (valid until the next call)."""
     import numpy as np
     import torch
     if dist is None:
         return proofs
-    lens = np.array([len(p) for p in proofs], dtype=np.int64)
+    X = _Exchange
     hdr = 8 * per_rank
-    size = torch.tensor([hdr + int(lens.sum())], dtype=torch.int64, device=device)
+    if hasattr(proofs, "packed_into"):
+        cap = hdr + per_rank * proofs._cap
+    else:
+        cap = hdr + sum(len(p) for p in proofs)
+    if X.send is None or X.send[0].numel() < cap:
+        X.send = [_pinned(cap + (1 << 20), device), _pinned(cap + (1 << 20), device)]
+    X.flip ^= 1
+    rec = X.send[X.flip]
+    buf = rec.numpy()
+    if hasattr(proofs, "packed_into"):
+        mine = proofs.packed_into(buf)
+    else:
+        lens = np.array([len(p) for p in proofs], dtype=np.int64)
+        buf[:hdr] = lens.view(np.uint8)
+        off = hdr
+        for p in proofs:  # one copy of each proof, straight into the record
+            buf[off:off + len(p)] = np.frombuffer(p, dtype=np.uint8)
+            off += len(p)
+        mine = off
+    size = torch.tensor([mine], dtype=torch.int64, device=device)
     dist.all_reduce(size, op=dist.ReduceOp.MAX)
-    payload = np.zeros(int(size.item()), dtype=np.uint8)
-    payload[:hdr] = lens.view(np.uint8)
-    off = hdr
-    for p in proofs:  # one copy of each proof, straight into the payload
-        payload[off:off + len(p)] = np.frombuffer(p, dtype=np.uint8)
-        off += len(p)
-    t = torch.from_numpy(payload).to(device)
-    got = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
+    size = int(size.item())
+    t = rec[:size].to(device, non_blocking=True) if device.type == "cuda" else rec[:size]
+    got = None
+    if rank == 0:
+        if X.big is None or X.big.shape[0] != world or X.big.shape[1] < size:
+            X.big = torch.empty((world, size + (1 << 20)), dtype=torch.uint8, device=device)
+        got = [X.big[r, :size] for r in range(world)]
     dist.gather(t, got, dst=0)
     if rank != 0:
         return None
-    stacked = torch.stack(got)
-    if stacked.is_cuda:  # one D2H into a reused pinned buffer
-        pin = getattr(gather_proofs, "_pin", None)
-        if pin is None or pin.numel() < stacked.numel():
-            pin = torch.empty(stacked.numel() + (1 << 20), dtype=torch.uint8, pin_memory=True)
-            gather_proofs._pin = pin
-        host = pin[:stacked.numel()].view(stacked.shape)
-        host.copy_(stacked)
+    if device.type == "cuda":  # one D2H of all ranks' records into a reused pinned buffer
+        if X.host is None or X.host.numel() < world * size:
+            X.host = _pinned(world * size + (8 << 20), device)
+        host = X.host[:world * size].view(world, size)
+        host.copy_(X.big[:, :size])
         allb = host.numpy()
     else:
-        allb = stacked.numpy()
+        allb = X.big[:, :size].numpy()
     out = []
     for r in range(world):
         row = allb[r]
@@ -387,6 +419,8 @@ def main():
         return prover.submit_batch(kws, trace_length=n)
 
     def collect_fn(pending):
+        if dist is not None:  # packed straight into the exchange record by gather_proofs
+            return pending
         res = pending.result()
         for r in res:
             if isinstance(r, Exception):

@@ -55,7 +55,8 @@ def test_lde_kernel_matches_oracle(prover, n, blowup):
         assert [int(v) for v in got[p]] == want
 
 
-@pytest.mark.parametrize("n,blowup", [(1 << 18, 2), (1 << 22, 2), (1 << 20, 16), (1 << 22, 4)])
+@pytest.mark.parametrize("n,blowup", [(1 << 18, 2), (1 << 22, 2), (1 << 20, 16), (1 << 22, 4), (1 << 16, 4),
+                                      (1 << 16, 16), (1 << 17, 8), (1 << 17, 16)])
 def test_lde_kernel_tile_paths_match_oracle(prover, n, blowup):
     """the remaining four-step shapes: 2^18 (R = 256 narrow tiles, C = 1024 with 512-thread pass B
     tiles) and 2^22 (R = 1024 wide 1024-thread pass A, C = 4096 narrow pass B), one polynomial,

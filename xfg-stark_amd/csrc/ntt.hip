@@ -87,7 +87,10 @@ __device__ __forceinline__ u64 tw_get(const Tables& T, int k, u64 e, bool inv) {
 // outputs of a group, which belong at logical positions base + r * stride.
 // IN_PLACE: every load of the step completes (barrier) before any store.
 // pf(q, seq, base, stride) runs before the group's loads (prefetch of what st will need).
-template <int LOGS, int LOGR, int LOGE, bool INV, bool SEQ_FAST, bool IN_PLACE, int NT, class LD, class ST, class PF>
+// TW2D: the twiddle of element r of a group with k = j % Ns is ltw[r * Ns + k] (a per-step [r][k]
+// table, ntt_pass_a_cos2) instead of w^(r k step) = ltw[r * k * step]
+template <int LOGS, int LOGR, int LOGE, bool INV, bool SEQ_FAST, bool IN_PLACE, int NT, class LD, class ST, class PF,
+          bool TW2D = false>
 __device__ __forceinline__ void stockham(int lognseq, int Ns, const u64* ltw, LD ld, ST st, PF pf) {
     constexpr int S = 1 << LOGS, R = 1 << LOGR, G = S / R, PER = (1 << LOGE) / R;
     const int nseq = 1 << lognseq;
@@ -107,7 +110,7 @@ __device__ __forceinline__ void stockham(int lognseq, int Ns, const u64* ltw, LD
         if (Ns > 1) {
             const int k = j % Ns, step = S / (Ns * R);
 #pragma unroll
-            for (int r = 1; r < R; r++) v[q][r] = gl_mul(v[q][r], ltw[r * k * step]);
+            for (int r = 1; r < R; r++) v[q][r] = gl_mul(v[q][r], TW2D ? ltw[r * Ns + k] : ltw[r * k * step]);
         }
         dft_reg<LOGR, INV>(v[q]);
         gs[q] = g0 < groups ? seq : -1;
@@ -144,7 +147,7 @@ struct Plan {
 // LDS tile, the last step stores with stg (global). A one-step DFT goes global -> global.
 // stg(q, seq, base, stride, v) stores group q's outputs; pf as in stockham, for the last step
 constexpr int NT_LOG2(int nt) { return nt <= 1 ? 0 : 1 + NT_LOG2(nt / 2); }
-template <int LOGS, int LOGE, bool INV, bool FIRST_SEQ_FAST, int NT, class LDG, class STG, class PF>
+template <int LOGS, int LOGE, bool INV, bool FIRST_SEQ_FAST, int NT, class LDG, class STG, class PF, bool TW2D_LAST = false>
 __device__ __forceinline__ void pass_dft(u64* tile, int lognseq, const u64* ltw, LDG ldg, STG stg, PF pf) {
     using PL = Plan<LOGS, LOGE>;
     constexpr int L = NT_LOG2(NT) + LOGE - LOGS;
@@ -167,6 +170,7 @@ __device__ __forceinline__ void pass_dft(u64* tile, int lognseq, const u64* ltw,
             nopf);
         __syncthreads();
         int Ns = 1 << PL::FIRST_LOGR;
+        auto ldl = [&](int seq, int j, int o) { return tile[seq * PITCH + phys2<LOGE>(j, o)]; };
 #pragma unroll
         for (int st = 1; st < PL::NSTEP - 1; st++) {
             stockham<LOGS, LOGE, LOGE, INV, true, true, NT>(
@@ -180,8 +184,8 @@ __device__ __forceinline__ void pass_dft(u64* tile, int lognseq, const u64* ltw,
             __syncthreads();
             Ns <<= LOGE;
         }
-        stockham<LOGS, PL::LAST_LOGR, LOGE, INV, true, false, NT>(
-            lognseq, Ns, ltw, [&](int seq, int j, int o) { return tile[seq * PITCH + phys2<LOGE>(j, o)]; }, stg, pf);
+        stockham<LOGS, PL::LAST_LOGR, LOGE, INV, true, false, NT, decltype(ldl), STG, PF, TW2D_LAST>(lognseq, Ns, ltw,
+                                                                                                ldl, stg, pf);
         __syncthreads();
     }
 }
@@ -379,6 +383,78 @@ __global__ __launch_bounds__(256, 3) void ntt_pass_a_cos(NttArgs a) {
     }
 }
 
+// ---------------------------------------------------------------- pass A, all cosets, shift twists
+// ntt_pass_a_cos without the per-coset pre-factor multiply. The pre-factor of coset t at column
+// row j1 = j0 + 16 r (first-step group j0, element r) splits as
+//   7^(C j1) w_(beta R)^(t j1) = [7^(C j0) w_(beta R)^(t j0)] * [7^(16 C r) w_(16 beta)^(t r)]:
+// the group factor is the same for a group's 16 elements, so it rides on the second step's twiddle
+// (a per-coset [r][k] table: w_R^(r k) times the factor of group r); of the element factor, with
+// t = M k + c (M = beta / 4 classes), w_(16 beta)^(t r) = w_(16 beta)^(c r) w_64^(k r), and w_64 = 2^39
+// is a shift. So each class starts from the coefficients times 7^(16 C r) w_(16 beta)^(c r) (one
+// multiply per element per class) and advances from coset to coset of its class by w_64^r (a
+// shift multiply): one general multiply per output becomes ~3/4 shift + M/beta general.
+// Cosets run class by class; every coset's column DFTs are otherwise those of ntt_pass_a_cos.
+// Forward LDE with the four-step table, beta in {4, 8, 16}, R = 256 (256 x 16 tiles of 16 columns).
+struct NoPf {
+    __device__ void operator()(int, int, int, int) const {}
+};
+template <int R_>
+__device__ __forceinline__ u64 mul_w64pow(u64 x) {  // x * w_64^R_ = x * 2^(39 R_ mod 192)
+    constexpr int e = (39 * R_) % 192;
+    if constexpr (e == 0) return x;
+    else if constexpr (e < 96) return mul_pow2<e>(x);
+    else return mul_pow2<e - 96>(P - x);  // 2^96 = -1; P - x is -x for any canonical x
+}
+__global__ __launch_bounds__(256, 4) void ntt_pass_a_cos2(NttArgs a) {
+    constexpr int LOGR = 8, LOGT = 8, LOGE = 4, NT = 1 << LOGT, R = 1 << LOGR, PITCH = row_pitch(R);
+    using PL = Plan<LOGR, LOGE>;
+    constexpr int R1 = 1 << PL::FIRST_LOGR, G1 = R / R1, RR = PL::LAST_R;
+    static_assert(R1 == 16 && G1 == 16 && RR == 16 && PL::NSTEP == 2, "16 x 16 column DFTs");
+    extern __shared__ u64 lds[];
+    const int logTC = (a.logC < LOGT + LOGE - LOGR) ? a.logC : LOGT + LOGE - LOGR;
+    const int TC = 1 << logTC;
+    u64* tile = lds;
+    u64* comb = lds + TC * PITCH;  // [r][k] second-step twiddles of the current coset
+    const int poly = blockIdx.y, col0 = blockIdx.x * TC;
+    const u64 n = 1ULL << a.logn;
+    const int beta = 1 << a.logbeta, M = beta >> 2, KP = beta / M;
+    const u64* comb_all = a.pt + R + (1 << a.logC) + ((u64)R << a.logbeta);  // [t][16][16]
+    const u64* scal = comb_all + ((u64)R << a.logbeta);                        // [c][16]
+    const int g = threadIdx.x, seq0 = g & (TC - 1), j0 = g >> logTC;
+    const auto rin = buf_rsrc(a.in + (u64)poly * a.in_stride + col0);
+    u64 cnext = comb_all[threadIdx.x];  // coset 0's table (class 0, k = 0)
+    for (int c = 0; c < M; c++) {
+        // the coefficients are (re)loaded per class -- from L2 after the first class -- rather than
+        // kept in registers: 32 VGPRs fewer, 4 waves per SIMD instead of 3
+        u64 cur[R1];
+#pragma unroll
+        for (int r = 0; r < R1; r++) cur[r] = buf_ld(rin, (((u32)j0 << a.logC) + seq0) * 8, ((u32)(r * G1) << a.logC) * 8);
+#pragma unroll
+        for (int r = 0; r < R1; r++) cur[r] = gl_mul(cur[r], scal[c * R1 + r]);
+        for (int k = 0; k < KP; k++) {
+            const int t = M * k + c, pt = poly * beta + t;
+            // (the previous coset's last step has passed its barrier; only this coset's second step,
+            // behind the barrier between the two steps, reads the table)
+            comb[threadIdx.x] = cnext;
+            const int tn = k + 1 < KP ? t + M : c + 1;  // next coset in processing order
+            if (tn < beta) cnext = comb_all[(tn << 8) + threadIdx.x];
+            const auto ry = buf_rsrc(a.y + (u64)pt * n + col0);
+            auto ldg = [&](int, int, int o) -> u64 { return cur[o / G1]; };
+            auto stg = [&](int, int seq, int base, int stride, u64* v) {
+                const u32 vo = (((u32)base << a.logC) + seq) * 8;
+#pragma unroll
+                for (int r = 0; r < RR; r++) buf_st(ry, vo, ((u32)(r * stride) << a.logC) * 8, v[r]);
+            };
+            pass_dft<LOGR, LOGE, false, true, NT, decltype(ldg), decltype(stg), NoPf, true>(tile, logTC, comb, ldg, stg,
+                                                                                           NoPf{});  // ends with a barrier
+            if (k + 1 < KP) static_for<R1>([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                cur[r] = mul_w64pow<r>(cur[r]);
+            });
+        }
+    }
+}
+
 // ---------------------------------------------------------------- pass B: row DFTs (size C)
 template <int LOGC, bool INV, int LOGT, int LOGE>
 __global__ __launch_bounds__(1 << LOGT) void ntt_pass_b(NttArgs a) {
@@ -466,8 +542,10 @@ __global__ __launch_bounds__(1 << LOGT) void ntt_pass_b(NttArgs a) {
 // Tiles are dealt per XCD in contiguous ranges (the blocks of XCD x = blockIdx % 8 walk the x-th
 // eighth of the tiles side by side), so the 64-byte output runs of neighbouring tiles meet in
 // one L2, as xcd_block arranges for the one-tile form.
-template <int LOGC, int LOGT, int LOGE>
-__global__ __launch_bounds__(1 << LOGT, 2) void ntt_pass_b_pers(NttArgs a, int ntx, int ntiles) {
+template <int LOGC, int LOGT, int LOGE, int TQ, int MINW>
+__global__ __launch_bounds__(1 << LOGT, MINW) void ntt_pass_b_pers(NttArgs a, int ntx, int ntiles) {
+    // TQ: 0 no four-step table (configs[4]); 1 table twiddles loaded per tile; 2 table twiddles
+    // prefetched with the data (the four-step table has the intermediate's [k1][j2] layout)
     constexpr int C = 1 << LOGC, RR = Plan<LOGC, LOGE>::LAST_R, NT = 1 << LOGT;
     using PLB = Plan<LOGC, LOGE>;
     constexpr int R1 = 1 << PLB::FIRST_LOGR, G1 = C / R1;
@@ -485,20 +563,39 @@ __global__ __launch_bounds__(1 << LOGT, 2) void ntt_pass_b_pers(NttArgs a, int n
     const int per_x = gridDim.x >> 3, x = blockIdx.x & 7, slot = blockIdx.x >> 3;
     const int span = (ntiles + 7) >> 3, tend = min((x + 1) * span, ntiles);
     const int seq0 = threadIdx.x / G1, j0 = threadIdx.x % G1;
-    auto load = [&](int ti, u64* dst) {
+    const int bmask = (1 << a.logbeta) - 1;
+    auto load = [&](int ti, u64* dst, u64* tdst) {
         const int pt = ti / ntx, k10 = (ti - pt * ntx) * TR;
-        const u64* y = a.y + (u64)pt * n + ((u64)(k10 + seq0) << LOGC) + j0;
+        const u64 i0 = ((u64)(k10 + seq0) << LOGC) + j0;
+        const u64* y = a.y + (u64)pt * n + i0;
 #pragma unroll
         for (int r = 0; r < R1; r++) dst[r] = y[r * G1];
+        if constexpr (TQ != 0) {
+            const u64* tq = a.t4 + ((u64)(pt & bmask) << a.logn) + i0;
+#pragma unroll
+            for (int r = 0; r < R1; r++) tdst[r] = tq[r * G1];
+        }
     };
     int ti = x * span + slot;
-    u64 yv[R1];
-    if (ti < tend) load(ti, yv);
+    u64 yv[R1], tv[TQ ? R1 : 1];
+    if (ti < tend) load(ti, yv, tv);
     for (; ti < tend; ti += per_x) {
         const int pt = ti / ntx, k10 = (ti - pt * ntx) * TR;
-        u64 nx[R1];
-        if (ti + per_x < tend) load(ti + per_x, nx);
-        auto ldg = [&](int, int, int o) -> u64 { return yv[o / G1]; };
+        u64 nx[R1], ntq[TQ == 2 ? R1 : 1];
+        if (ti + per_x < tend) {
+            if constexpr (TQ == 2) load(ti + per_x, nx, ntq);
+            else {
+                const u64* y = a.y + (u64)((ti + per_x) / ntx) * n;
+                const int k1n = ((ti + per_x) % ntx) * TR;
+                const u64 i0 = ((u64)(k1n + seq0) << LOGC) + j0;
+#pragma unroll
+                for (int r = 0; r < R1; r++) nx[r] = y[i0 + r * G1];
+            }
+        }
+        auto ldg = [&](int, int, int o) -> u64 {
+            if constexpr (TQ != 0) return gl_mul(yv[o / G1], tv[o / G1]);
+            return yv[o / G1];
+        };
         const auto rout = buf_rsrc(a.out + (u64)pt * n + k10);
         auto stg = [&](int, int seq, int base, int stride, u64* v) {
 #pragma unroll
@@ -508,6 +605,17 @@ __global__ __launch_bounds__(1 << LOGT, 2) void ntt_pass_b_pers(NttArgs a, int n
         pass_dft<LOGC, LOGE, false, false, NT>(tile, logTR, ltw, ldg, stg, [](int, int, int, int) {});
 #pragma unroll
         for (int r = 0; r < R1; r++) yv[r] = nx[r];
+        if constexpr (TQ == 2) {
+#pragma unroll
+            for (int r = 0; r < R1; r++) tv[r] = ntq[r];
+        } else if constexpr (TQ == 1) {
+            if (ti + per_x < tend) {
+                const int pn = (ti + per_x) / ntx, k1n = ((ti + per_x) % ntx) * TR;
+                const u64* tq = a.t4 + ((u64)(pn & bmask) << a.logn) + ((u64)(k1n + seq0) << LOGC) + j0;
+#pragma unroll
+                for (int r = 0; r < R1; r++) tv[r] = tq[r * G1];
+            }
+        }
     }
 }
 
@@ -666,12 +774,28 @@ __global__ void pass_tables_kernel(u64* out, int logn, int logbeta, int logR, in
     } else if (!inv && i < R + C + (R << logbeta)) {
         const u64 t = (i - R - C) >> logR, j = (i - R - C) & (R - 1);
         out[i] = gl_mul(T.pow7[j << logC], tw_get(T, logR + logbeta, (t * j) & ((1ULL << (logR + logbeta)) - 1), false));
+    } else if (!inv && logR == 8 && logbeta >= 2) {
+        // ntt_pass_a_cos2: [t][r][k] = w_R^(r k) 7^(C r) w_(beta R)^(t r), then [c][r] = 7^(16 C r) w_(16 beta)^(c r)
+        const u64 q = i - R - C - (R << logbeta);
+        const u64 M = 1ULL << (logbeta - 2);
+        if (q < (R << logbeta)) {
+            const u64 t = q >> 8, r = (q >> 4) & 15, k = q & 15;
+            const u64 grp = gl_mul(T.pow7[r << logC], tw_get(T, logR + logbeta, (t * r) & ((1ULL << (logR + logbeta)) - 1), false));
+            out[i] = gl_mul(tw_get(T, logR, r * k, false), grp);
+        } else if (q < (R << logbeta) + 16 * M) {
+            const u64 c = (q - (R << logbeta)) >> 4, r = q & 15;
+            out[i] = gl_mul(T.pow7[(16 * r) << logC], tw_get(T, 4 + logbeta, (c * r) & ((1ULL << (4 + logbeta)) - 1), false));
+        }
     }
+}
+// entries of the ntt_pass_a_cos2 tables appended to the forward pass tables (R = 256, beta >= 4)
+static u64 cos2_extra(int logR, int logbeta) {
+    return (logbeta >= 0 && logR == 8 && logbeta >= 2) ? ((1ULL << (logR + logbeta)) + (16ULL << (logbeta - 2))) : 0;
 }
 u64 pass_tables_size(int logn, int logbeta) {
     int logR, logC;
     ntt_split(logn, logR, logC);
-    return (1ULL << logR) + (1ULL << logC) + (logbeta >= 0 ? (1ULL << (logR + logbeta)) : 0);
+    return (1ULL << logR) + (1ULL << logC) + (logbeta >= 0 ? (1ULL << (logR + logbeta)) : 0) + cos2_extra(logR, logbeta);
 }
 void build_pass_tables(u64* out, int logn, int logbeta, const Tables& T, hipStream_t s) {
     int logR, logC;
@@ -684,7 +808,8 @@ __host__ __device__ u64 fourstep_main(int logn, int logbeta) { return 1ULL << (l
 u64 fourstep_size(int logn, int logbeta) {
     int logR, logC;
     ntt_split(logn, logR, logC);
-    return fourstep_main(logn, logbeta) + (1ULL << logR) + (1ULL << logC) + (logbeta >= 0 ? (1ULL << (logR + logbeta)) : 0);
+    return fourstep_main(logn, logbeta) + (1ULL << logR) + (1ULL << logC) + (logbeta >= 0 ? (1ULL << (logR + logbeta)) : 0) +
+           cos2_extra(logR, logbeta);
 }
 void build_fourstep(u64* out, int logn, int logbeta, const Tables& T, hipStream_t s) {
     int logR, logC;
@@ -781,7 +906,15 @@ static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
             const char* v = getenv("XFG_NTT_COS");
             return !(v && *v == '0');
         }();
-        if (cos_on && a.t4 && a.logR == 8 && ltA == 8 && eA == 4 && !(a.xcd & 1)) {
+        // shift-twisted cosets (ntt_pass_a_cos2) where its tables exist; XFG_NTT_COS2=0 disables
+        static const bool cos2_on = [] {
+            const char* v = getenv("XFG_NTT_COS2");
+            return !(v && *v == '0');
+        }();
+        if (cos_on && cos2_on && a.t4 && a.logR == 8 && ltA == 8 && eA == 4 && !(a.xcd & 1) && a.logbeta >= 2) {
+            a.tq_b = 1;
+            hipLaunchKernelGGL(ntt_pass_a_cos2, dim3(C >> logTC, npoly), dim3(256), lds_a, s, a);
+        } else if (cos_on && a.t4 && a.logR == 8 && ltA == 8 && eA == 4 && !(a.xcd & 1)) {
             a.tq_b = 1;
             hipLaunchKernelGGL(ntt_pass_a_cos<8>, dim3(C >> logTC, npoly), dim3(256), lds_a, s, a);
         } else
@@ -791,12 +924,30 @@ static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
             const char* v = getenv("XFG_NTT_BPERS");
             return !(v && *v == '0');
         }();
+        // XFG_NTT_BPERS16: 0 = one tile per block at n = 2^16 (default), 1 / 2 = persistent with the
+        // table twiddles loaded per tile / prefetched (A/B knob)
+        static const int bpers16 = [] {
+            const char* v = getenv("XFG_NTT_BPERS16");
+            return v && *v ? atoi(v) : 0;
+        }();
+        int dev = 0, cus = 256;
+        auto ncu = [&] {
+            if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            return cus;
+        };
         if (bpers_on && eB == 5 && ltB == 8 && a.logC == 10 && a.logR >= 3 && !a.t4 && a.pt && !a.yblk) {
             const int ntx = R >> logTR, ntiles = ntx * npoly * ncos;
-            int dev = 0, cus = 256;
-            if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            const int nb = std::max(8, std::min(2 * cus, ntiles) & ~7);
-            hipLaunchKernelGGL((ntt_pass_b_pers<10, 8, 5>), dim3(nb), dim3(256), lds_b, s, a, ntx, ntiles);
+            const int nb = std::max(8, std::min(2 * ncu(), ntiles) & ~7);
+            hipLaunchKernelGGL((ntt_pass_b_pers<10, 8, 5, 0, 2>), dim3(nb), dim3(256), lds_b, s, a, ntx, ntiles);
+        } else if (bpers16 && eB == 4 && ltB == 8 && a.logC == 8 && a.logR >= 4 && a.t4 && a.tq_b && a.pt) {
+            const int ntx = R >> logTR, ntiles = ntx * npoly * ncos;
+            if (bpers16 == 2) {
+                const int nb = std::max(8, std::min(3 * ncu(), ntiles) & ~7);
+                hipLaunchKernelGGL((ntt_pass_b_pers<8, 8, 4, 2, 3>), dim3(nb), dim3(256), lds_b, s, a, ntx, ntiles);
+            } else {
+                const int nb = std::max(8, std::min(4 * ncu(), ntiles) & ~7);
+                hipLaunchKernelGGL((ntt_pass_b_pers<8, 8, 4, 1, 4>), dim3(nb), dim3(256), lds_b, s, a, ntx, ntiles);
+            }
         } else
             run_pass_b<false>(a.logC, ltB, eB, gb, lds_b, s, a);
     }

@@ -366,6 +366,39 @@ class PendingBatch:
             self._res = res
         return self._res
 
+    def packed_into(self, dst):
+        """wait, then write the batch as one record into the uint8 numpy array `dst`: count int64
+        lengths followed by the proof bytes back to back (the exchange format of a sharded run,
+        bench.gather_proofs), straight from the workers' output buffer -- no per-proof bytes
+        objects. Returns the record size. Any per-proof error raises."""
+        import numpy as np
+        if self._res is None:
+            st = _lib.xfg_batch_wait(self._p._ctx, self._t)
+            if st:
+                self._p._free.append(self._buf)
+                self._res = []
+                raise self._p._err(st)
+            k = len(self._sts)
+            bad = [i for i in range(k) if self._sts[i]]
+            lens = np.array([self._lens[i] for i in range(k)], dtype=np.int64)
+            hdr = 8 * k
+            need = hdr + int(lens.sum())
+            if bad or need > dst.size:
+                self._p._free.append(self._buf)
+                self._res = []
+                if bad:
+                    raise XfgStarkError(self._sts[bad[0]], STATUS.get(self._sts[bad[0]]))
+                raise XfgStarkError(8, "packed_into: destination too small")
+            dst[:hdr] = lens.view(np.uint8)
+            base, off = dst.ctypes.data, hdr
+            for i in range(k):
+                C.memmove(base + off, self._base + i * self._cap, int(lens[i]))
+                off += int(lens[i])
+            self._p._free.append(self._buf)
+            self._res = []  # consumed: result() is not available after packed_into
+            return need
+        raise XfgStarkError(9, "packed_into after result(): the batch's buffer was released")
+
     def __del__(self):
         # the workers write into this batch's buffers: never release them before the batch is done
         if self._res is None and getattr(self._p, "_ctx", None):
