@@ -48,8 +48,9 @@ def pack_inputs(kws):
 
 def unpack_inputs(arr):
     res = []
-    for r in arr:
-        b = bytes(r.tolist())
+    raw = arr.tobytes()  # one copy; records sliced from it
+    for i in range(len(arr)):
+        b = raw[i * REC:(i + 1) * REC]
         res.append(dict(burn_amount=int.from_bytes(b[0:8], "little"), mint_amount=int.from_bytes(b[8:16], "little"),
                         tx_prefix_hash=b[16:48], recipient_address=b[48:68], secret=b[68:100],
                         network_id=int.from_bytes(b[100:104], "little"),
