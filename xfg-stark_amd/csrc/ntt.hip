@@ -533,6 +533,50 @@ __global__ __launch_bounds__(1 << LOGT) void ntt_pass_b(NttArgs a) {
                                                                    [](int, int, int, int) {});
 }
 
+// ---------------------------------------------------------------- pass B, forward with the four-step table
+// ntt_pass_b specialised to the path every tabled LDE takes (the all-coset pass A left the four-step
+// twiddles to it): one first-step group per thread, data and table loaded up front, no run-time
+// branches for the other paths
+template <int LOGC, int LOGT, int LOGE>
+__global__ __launch_bounds__(1 << LOGT) void ntt_pass_b_tq(NttArgs a) {
+    constexpr int C = 1 << LOGC, RR = Plan<LOGC, LOGE>::LAST_R, NT = 1 << LOGT;
+    using PLB = Plan<LOGC, LOGE>;
+    constexpr int R1 = 1 << PLB::FIRST_LOGR, G1 = C / R1;
+    static_assert(PLB::NSTEP > 1 && (1 << LOGE) == R1, "one full-radix first-step group per thread");
+    extern __shared__ u64 lds[];
+    const int logTR = (a.logR < LOGT + LOGE - LOGC) ? a.logR : LOGT + LOGE - LOGC;
+    const int TR = 1 << logTR;
+    u64* tile = lds;
+    u64* ltw = lds + TR * row_pitch(C, LOGE, LOGT + LOGE - LOGC);
+    int bx, by;
+    xcd_block(a.xcd & 2, bx, by);
+    const int pt = by, k10 = bx * TR;
+    const u64 n = 1ULL << a.logn;
+    {
+        const u64* pt4 = a.pt + (1 << a.logR);
+        for (int i = threadIdx.x; i < C; i += NT) ltw[i] = pt4[i];
+    }
+    const int seq0 = threadIdx.x / G1, j0 = threadIdx.x % G1;
+    const u64 i0 = ((u64)(k10 + seq0) << LOGC) + j0;
+    const u64* y = a.y + (u64)pt * n + i0;
+    const u64* tq = a.t4 + ((u64)(pt & ((1 << a.logbeta) - 1)) << a.logn) + i0;
+    u64 yv[R1], tv[R1];
+#pragma unroll
+    for (int r = 0; r < R1; r++) {
+        yv[r] = y[r * G1];
+        tv[r] = tq[r * G1];
+    }
+    __syncthreads();
+    auto ldg = [&](int, int, int o) -> u64 { return gl_mul(yv[o / G1], tv[o / G1]); };
+    const auto rout = buf_rsrc(a.out + (u64)pt * n + k10);
+    auto stg = [&](int, int seq, int base, int stride, u64* v) {
+#pragma unroll
+        for (int r = 0; r < RR; r++)
+            buf_st(rout, (seq + ((u32)base << a.logR)) * 8, ((u32)(r * stride) << a.logR) * 8, canon(v[r]));
+    };
+    pass_dft<LOGC, LOGE, false, false, NT>(tile, logTR, ltw, ldg, stg, NoPf{});
+}
+
 // ---------------------------------------------------------------- pass B, persistent (forward, no table)
 // The row DFTs of an LDE past the four-step tables (configs[4]: 2^24 points, radix 32 x 32, 8 rows
 // per tile, two blocks per CU). One tile per block waited on its loads for 48 % of its wave cycles
@@ -924,6 +968,11 @@ static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
             const char* v = getenv("XFG_NTT_BPERS");
             return !(v && *v == '0');
         }();
+        // specialised tabled pass B (XFG_NTT_TQSPEC=0 disables, for A/B runs)
+        static const bool tqspec_on = [] {
+            const char* v = getenv("XFG_NTT_TQSPEC");
+            return !(v && *v == '0');
+        }();
         // XFG_NTT_BPERS16: 0 = one tile per block at n = 2^16 (default), 1 / 2 = persistent with the
         // table twiddles loaded per tile / prefetched (A/B knob)
         static const int bpers16 = [] {
@@ -939,6 +988,9 @@ static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
             const int ntx = R >> logTR, ntiles = ntx * npoly * ncos;
             const int nb = std::max(8, std::min(2 * ncu(), ntiles) & ~7);
             hipLaunchKernelGGL((ntt_pass_b_pers<10, 8, 5, 0, 2>), dim3(nb), dim3(256), lds_b, s, a, ntx, ntiles);
+        } else if (!bpers16 && tqspec_on && eB == 4 && ltB == 8 && a.logC == 8 && a.logR >= 4 && a.t4 && a.tq_b && a.pt &&
+                   !a.yblk) {
+            hipLaunchKernelGGL((ntt_pass_b_tq<8, 8, 4>), gb, dim3(256), lds_b, s, a);  // lds_b < 64 KiB here
         } else if (bpers16 && eB == 4 && ltB == 8 && a.logC == 8 && a.logR >= 4 && a.t4 && a.tq_b && a.pt) {
             const int ntx = R >> logTR, ntiles = ntx * npoly * ncos;
             if (bpers16 == 2) {
