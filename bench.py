@@ -367,7 +367,7 @@ def verify_rate(prover, proofs, inputs, threads=16, reps=3):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--per-gpu", type=int, default=64)
     ap.add_argument("--log-n", type=int, default=LOG_N)
@@ -514,7 +514,7 @@ def main():
                          # the kernel is VALU-issue-bound: the same launch set
                          # against the VALU ceiling, instruction counts from the same PMC record
                          "valu": valu_roofline(pmc, lde_ms, WIDTH * per * n * BLOWUP),
-                         "kernel": "trace LDE (ntt_pass_a_cos2 + ntt_pass_b<8,false,8,4>), 7 columns x "
+                         "kernel": "trace LDE (ntt_pass_a_cos2 + ntt_pass_b_tq<8,8,4>), 7 columns x "
                                    f"{per} proofs, {lde_ms:.3f} ms/launch-set, {lde_bytes} algorithmic B",
                          # the same launch sets inside the timed pipelined steps (per XFG_UNIT-proof unit,
                          # sharing the GPU with the other lanes' kernels)

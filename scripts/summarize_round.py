@@ -35,7 +35,7 @@ for e in ev:
 sel = {}
 for k in ("a", "b"):
     cand = [(g, nm) for (kk, nm, g) in big if kk == k and "cos" in nm] if k == "a" else \
-           [(g, nm) for (kk, nm, g) in big if kk == k and "<8, false, 8, 4>" in nm]
+           [(g, nm) for (kk, nm, g) in big if kk == k and ("<8, false, 8, 4>" in nm or "ntt_pass_b_tq" in nm)]
     if cand:
         sel[k] = max(cand)
 if len(sel) == 2:

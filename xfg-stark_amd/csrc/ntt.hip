@@ -984,7 +984,7 @@ static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
             if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
             return cus;
         };
-        if (bpers_on && eB == 5 && ltB == 8 && a.logC == 10 && a.logR >= 3 && !a.t4 && a.pt && !a.yblk) {
+        if (bpers_on && eB == 5 && ltB == 8 && a.logC == 10 && a.logR >= 3 && !a.tq_b && a.pt && !a.yblk) {
             const int ntx = R >> logTR, ntiles = ntx * npoly * ncos;
             const int nb = std::max(8, std::min(2 * ncu(), ntiles) & ~7);
             hipLaunchKernelGGL((ntt_pass_b_pers<10, 8, 5, 0, 2>), dim3(nb), dim3(256), lds_b, s, a, ntx, ntiles);

@@ -402,10 +402,20 @@ static Tables tables_of(xfg_ctx* c) {
 // four-step twiddle tables of the NTT sizes one (n, beta) proof uses: the forward LDE and the
 // inverse NTTs of sizes 8 .. 2n (trace, composition, FRI remainder). Sizes whose table would exceed
 // 2^FOURSTEP_MAX_LOG entries keep the running-product twiddles. Returns false when one is missing.
+// largest log2(n beta) with a forward four-step table: FOURSTEP_MAX_LOG, or up to 24 with
+// XFG_FOURSTEP_MAX (A/B knob: configs[4]'s 2^24-point LDE with a 128 MiB table)
+static int fwd_table_max_log() {
+    static const int v = [] {
+        const char* e = getenv("XFG_FOURSTEP_MAX");
+        const int x = e && *e ? atoi(e) : FOURSTEP_MAX_LOG;
+        return std::min(std::max(x, FOURSTEP_MAX_LOG), 24);
+    }();
+    return v;
+}
 static bool fourstep_ready(xfg_ctx* c, int logn, int logbeta) {
     const FourStep& f = c->tables.fs;
-    if (logn + logbeta <= FOURSTEP_MAX_LOG && !f.fwd[logn][logbeta]) return false;
-    if (logn + logbeta > FOURSTEP_MAX_LOG && logn <= PASS_MAX_LOG && !f.pass_fwd[logn][logbeta]) return false;
+    if (logn + logbeta <= fwd_table_max_log() && !f.fwd[logn][logbeta]) return false;
+    if (logn + logbeta > fwd_table_max_log() && logn <= PASS_MAX_LOG && !f.pass_fwd[logn][logbeta]) return false;
     for (int l = 3; l <= std::min(logn + 1, FOURSTEP_MAX_LOG); l++)
         if (!f.inv[l]) return false;
     return true;
@@ -422,8 +432,8 @@ static void ensure_fourstep(xfg_ctx* c, int logn, int logbeta) {
         return (const u64*)b.p;
     };
     FourStep& f = c->tables.fs;
-    if (logn + logbeta <= FOURSTEP_MAX_LOG && !f.fwd[logn][logbeta]) f.fwd[logn][logbeta] = build(logn, logbeta);
-    if (logn + logbeta > FOURSTEP_MAX_LOG && logn <= PASS_MAX_LOG && !f.pass_fwd[logn][logbeta]) {
+    if (logn + logbeta <= fwd_table_max_log() && !f.fwd[logn][logbeta]) f.fwd[logn][logbeta] = build(logn, logbeta);
+    if (logn + logbeta > fwd_table_max_log() && logn <= PASS_MAX_LOG && !f.pass_fwd[logn][logbeta]) {
         DBuf<u64>& b = c->tables.pass_buf[logn * 8 + logbeta];
         b.ensure(pass_tables_size(logn, logbeta));
         build_pass_tables(b.p, logn, logbeta, T, 0);
