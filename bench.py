@@ -166,13 +166,25 @@ def pipelined_steps(submit_fn, collect_fn, batches, rank, world, per_rank, devic
     (and the Python collection) overlaps the kernels of the next ones. Every step is proven in
     full; returns the last step's proofs on rank 0."""
     pending, out = [], None
+    tl = [] if os.environ.get("XFG_BENCH_TIMELINE") else None  # step completion times (stderr)
+    ts = []
+    t0 = time.perf_counter()
     for i, b in enumerate(batches):
         local = scatter_inputs(b, rank, world, per_rank, device, dist, packed[i] if packed else None)
         pending.append(submit_fn(local))
+        if tl is not None:
+            ts.append(time.perf_counter() - t0)
         if len(pending) >= depth:
             out = gather_proofs(collect_fn(pending.pop(0)), rank, world, per_rank, device, dist)
+            if tl is not None:
+                tl.append(time.perf_counter() - t0)
     while pending:
         out = gather_proofs(collect_fn(pending.pop(0)), rank, world, per_rank, device, dist)
+        if tl is not None:
+            tl.append(time.perf_counter() - t0)
+    if tl:
+        print("timeline ms: " + " ".join(f"{t * 1e3:.1f}" for t in tl), file=sys.stderr)
+        print("submitted ms: " + " ".join(f"{t * 1e3:.1f}" for t in ts), file=sys.stderr)
     return out
 
 

@@ -1044,12 +1044,24 @@ static Lane* lane0(xfg_ctx* c) {
     }
     return c->lanes[0].get();
 }
+// XFG_LANE_PRIO (A/B knob): 1 = the first XFG_PRIO_HIGH lanes (default 3) on high-priority streams,
+// 2 = priorities graded by lane index; 0 (default) = every lane at the default priority
+static int env_int(const char* name, int dflt);
+static int lane_priority(int l) {
+    static const int mode = env_int("XFG_LANE_PRIO", 0), high = env_int("XFG_PRIO_HIGH", 3);
+    int least = 0, greatest = 0;
+    if (!mode || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return 0;
+    if (mode == 1) return l < high ? greatest : least;
+    const int span = least - greatest;  // greatest is numerically smaller
+    return std::max(greatest, least - (span ? l % (span + 1) : 0));
+}
 static void ensure_lanes(xfg_ctx* c, size_t k) {
     lane0(c);
     while (c->lanes.size() < k) {
         c->lanes.emplace_back(new Lane());
         c->lanes.back()->lde_probe = c->lde_probe;
-        HIPCHK(hipStreamCreateWithFlags(&c->lanes.back()->stream, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithPriority(&c->lanes.back()->stream, hipStreamNonBlocking,
+                                           lane_priority((int)c->lanes.size() - 1)));
         for (auto& e : c->lanes.back()->ev) HIPCHK(hipEventCreate(&e));
     }
 }
