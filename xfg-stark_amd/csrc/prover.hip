@@ -23,6 +23,7 @@
 
 #include "../../include/xfg_stark.h"
 #include "host_common.hpp"
+#include "host_pool.hpp"
 #include "kernels.hpp"
 #include "verifier.hpp"
 
@@ -155,6 +156,7 @@ struct BW {
         memcpy(b.data() + end_of_slot - 4, &x, 4);
     }
     void finish(std::vector<uint8_t>& out) { out.assign(b.begin(), b.begin() + o); }
+    void trim() { b.resize(o); }  // the buffer is the output (the proof's own bytes)
 };
 
 // XFG_TRACE=1: host-side phase timestamps of every prove call (and any workspace reallocation,
@@ -260,6 +262,18 @@ enum {
     ST_COUNT
 };
 
+// one proof's opening plan (prove_lane step 7): the batch openings of the LDE trees and the FRI
+// layers, and its gather indices per source (values: trace LDE, composition LDE, FRI layers;
+// digests: trace / composition tree nodes, FRI layer nodes) and recomputed-subtree rows
+struct LaneLayout {
+    BatchOpening op;                     // trace / constraint trees (same positions)
+    std::vector<int64_t> ref;            // per node: >= 0 stored ordinal, < 0 -(open slot + 1), slots from this proof's first
+    std::vector<BatchOpening> fops;      // FRI layers
+    std::vector<std::vector<u64>> fpos;
+    std::vector<u64> vlde, vh, dt, dh, oent;
+    std::vector<std::vector<u64>> vf, df;
+};
+
 // one lane = one HIP stream + its pooled device buffers + one host thread; a batch is split
 // across lanes so one lane's host-side Fiat-Shamir / serialisation overlaps another's kernels
 struct Lane {
@@ -292,9 +306,8 @@ struct Lane {
     // host scratch of the opening plans and the serialiser, kept across units so steady-state
     // units neither allocate nor page-fault (their cost grew with the shared hosts' load)
     struct {
-        std::vector<u64> vidx_lde, vidx_h, didx_t, didx_h, open_ent, allidx;
-        std::vector<std::vector<u64>> vidx_f, didx_f;
-        std::vector<uint8_t> ser;
+        std::vector<u64> allidx;
+        std::vector<LaneLayout> lay;
     } hs;
     void release() {
         for (auto* b : {&h_roots, &h_gd}) b->release();
@@ -717,7 +730,9 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     ht.mark("sync_rem");
     // host replay of the transcript: commitments into the proof and the coin advanced exactly as the
     // device coin was; the device's coefficient, z and DEEP draws (and its rejections) must agree
-    for (int b = 0; b < B; b++) {
+    // (per proof, independent: spread over the host pool)
+    HostPool& pool = host_pool();
+    pool.parallel_for(B, [&](int b) {
         auto& j = jobs[b];
         bool failed = false, same = true;
         auto commit = [&](const Digest& r) {
@@ -762,39 +777,26 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         }
         if (failed) j.status = XFG_PROVER_ERROR;
         if (failed != (ffail[b] != 0) || !same) throw std::runtime_error("device / host transcript diverged");
-    }
+    });
 
     auto t_q0 = std::chrono::steady_clock::now();
     // ---- 7. grinding + query positions, gather lists
     // LDE trees store heap levels >= log2(beta) (indices < 2n); lower nodes of an opened row are
-    // recomputed by launch_open_rows (local heap: 2 * beta slots per row)
+    // recomputed by launch_open_rows (local heap: 2 * beta slots per row). Every proof's plan is
+    // built on its own (host pool) into per-proof index lists, which are then laid end to end.
     const u64 stored_lim = n, LB = beta;  // stored: heap levels >= log2(beta) + 1
-    auto& vidx_lde = c->hs.vidx_lde;
-    auto& vidx_h = c->hs.vidx_h;
-    auto& didx_t = c->hs.didx_t;
-    auto& didx_h = c->hs.didx_h;
-    auto& open_ent = c->hs.open_ent;
-    auto& vidx_f = c->hs.vidx_f;
-    auto& didx_f = c->hs.didx_f;
-    for (auto* v : {&vidx_lde, &vidx_h, &didx_t, &didx_h, &open_ent}) v->clear();
-    if (vidx_f.size() < nl + 1) {
-        vidx_f.resize(nl + 1);
-        didx_f.resize(nl + 1);
-    }
-    for (unsigned l = 0; l <= nl; l++) {
-        vidx_f[l].clear();
-        didx_f[l].clear();
-    }
-    struct Layout {
-        BatchOpening op;                     // trace / constraint trees (same positions)
-        std::vector<int64_t> ref;            // per node: >= 0 stored ordinal, < 0 -(open slot + 1)
-        std::vector<BatchOpening> fops;      // FRI layers
-        std::vector<std::vector<u64>> fpos;
-    };
-    std::vector<Layout> lay(B);
-    for (int b = 0; b < B; b++) {
+    using Layout = LaneLayout;
+    std::vector<Layout>& lay = c->hs.lay;
+    if (lay.size() < (size_t)B) lay.resize(B);
+    pool.parallel_for(B, [&](int b) {
         auto& j = jobs[b];
-        ht.tic();
+        Layout& L = lay[b];
+        L.ref.clear();
+        L.fops.clear();
+        L.fpos.clear();
+        for (auto* v : {&L.vlde, &L.vh, &L.dt, &L.dh, &L.oent}) v->clear();
+        L.vf.resize(nl);
+        L.df.resize(nl);
         if (dn2h[(size_t)b * DE] == 0 && dn2h[(size_t)b * DE + DE - 1] == 0)
             j.status = XFG_PROVER_ERROR;  // assert_eq!(trace_length - 2, degree)
         j.rem.resize(rem_len * DE);  // E elements, coordinates interleaved
@@ -819,12 +821,10 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         std::sort(pos.begin(), pos.end());
         pos.erase(std::unique(pos.begin(), pos.end()), pos.end());
         j.pos = pos;
-        ht.toc("q_grind_draw");
-        Layout& L = lay[b];
         for (u64 k : pos) {
             u64 t = k & (beta - 1), m = k >> logbeta;
-            for (int col = 0; col < 7; col++) vidx_lde.push_back((((u64)b * 7 + col) * beta + t) * n + m);
-            for (int k = 0; k < DE; k++) vidx_h.push_back((((u64)b * DE + k) * beta + t) * n + m);
+            for (int col = 0; col < 7; col++) L.vlde.push_back((((u64)b * 7 + col) * beta + t) * n + m);
+            for (int k = 0; k < DE; k++) L.vh.push_back((((u64)b * DE + k) * beta + t) * n + m);
         }
         // rows whose subtrees are recomputed: every queried row and its sibling row (the sibling's
         // subtree top, heap level log2(beta), is no longer stored)
@@ -835,64 +835,83 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         }
         std::sort(rows_b.begin(), rows_b.end());
         rows_b.erase(std::unique(rows_b.begin(), rows_b.end()), rows_b.end());
-        const u64 ent0 = open_ent.size();
-        for (u64 m : rows_b) open_ent.push_back(((u64)b << logn) | m);
+        for (u64 m : rows_b) L.oent.push_back(((u64)b << logn) | m);
         plan_batch_opening(pos, N, L.op);
         int64_t stored_ord = 0;
         L.op.each([&](u64 h) {
                 if (h < stored_lim) {
-                    didx_t.push_back((u64)b * 2 * n + h);
-                    didx_h.push_back((u64)b * 2 * n + h);
+                    L.dt.push_back((u64)b * 2 * n + h);
+                    L.dh.push_back((u64)b * 2 * n + h);
                     L.ref.push_back(stored_ord++);
                 } else {
+                    // open slot relative to this proof's first entry (rebased once the entries of
+                    // the proofs before it are counted)
                     unsigned lvl = (unsigned)(logn + logbeta) - (63 - __builtin_clzll(h));  // 0 = leaves
                     u64 off = h - (N >> lvl), span = logbeta - lvl;
                     u64 m = off >> span, local = (1ULL << span) + (off & ((1ULL << span) - 1));
-                    u64 e = ent0 + (std::lower_bound(rows_b.begin(), rows_b.end(), m) - rows_b.begin());
+                    u64 e = (u64)(std::lower_bound(rows_b.begin(), rows_b.end(), m) - rows_b.begin());
                     L.ref.push_back(-(int64_t)(e * 2 * LB + local) - 1);
                 }
             });
-        ht.toc("q_lde_plan");
         std::vector<u64> fp = pos;
         for (unsigned l = 0; l < nl; l++) {
             u64 rows = D[l] / 8;
             fp = fold_positions(fp, rows);
             L.fpos.push_back(fp);
+            auto& vf = L.vf[l];
+            vf.clear();
             for (u64 i : fp)
                 for (u64 k = 0; k < 8; k++) {
                     const u64 K = i + k * rows;
                     for (int cc = 0; cc < DE; cc++) {
                         if (l == 0)
-                            vidx_f[0].push_back((((u64)b * DE + cc) * beta + (K & (beta - 1))) * n + (K >> logbeta));
+                            vf.push_back((((u64)b * DE + cc) * beta + (K & (beta - 1))) * n + (K >> logbeta));
                         else
-                            vidx_f[l].push_back(((u64)b * DE + cc) * D[l] + K);
+                            vf.push_back(((u64)b * DE + cc) * D[l] + K);
                     }
                 }
             L.fops.emplace_back();
             plan_batch_opening(fp, rows, L.fops.back());
-            L.fops.back().each([&](u64 x) { didx_f[l].push_back((u64)b * 2 * rows + x); });
+            auto& df = L.df[l];
+            df.clear();
+            L.fops.back().each([&](u64 x) { df.push_back((u64)b * 2 * rows + x); });
         }
-        ht.toc("q_fri_plan");
-    }
+    });
     ht.mark("queries_plan");
-    // one index buffer, one value buffer, one digest buffer; segment per source
+    // one index buffer, one value buffer, one digest buffer; segment per source, the proofs' lists
+    // end to end inside each segment. cur_*[b]: where proof b's values / digests of a segment start
     auto& allidx = c->hs.allidx;
     allidx.clear();
+    const int NS = 2 + (int)nl;  // value segments: trace LDE, composition LDE, FRI layers (same count of digest segments)
     std::vector<std::pair<size_t, size_t>> vseg, dseg;  // (offset, count)
-    auto add_seg = [&](const std::vector<u64>& v, std::vector<std::pair<size_t, size_t>>& seg) {
-        seg.push_back({allidx.size(), v.size()});
-        allidx.insert(allidx.end(), v.begin(), v.end());
+    std::vector<size_t> vcur((size_t)NS * B), dcur((size_t)NS * B);
+    auto seg_of = [&](int k, bool dig, int b) -> const std::vector<u64>& {
+        const Layout& L = lay[b];
+        if (!dig) return k == 0 ? L.vlde : (k == 1 ? L.vh : L.vf[k - 2]);
+        return k == 0 ? L.dt : (k == 1 ? L.dh : L.df[k - 2]);
     };
-    add_seg(vidx_lde, vseg);
-    add_seg(vidx_h, vseg);
-    for (unsigned l = 0; l < nl; l++) add_seg(vidx_f[l], vseg);
-    size_t nvals = allidx.size();
-    add_seg(didx_t, dseg);
-    add_seg(didx_h, dseg);
-    for (unsigned l = 0; l < nl; l++) add_seg(didx_f[l], dseg);
+    for (int dig = 0; dig < 2; dig++)
+        for (int k = 0; k < NS; k++) {
+            auto& seg = dig ? dseg : vseg;
+            auto& cur = dig ? dcur : vcur;
+            seg.push_back({allidx.size(), 0});
+            for (int b = 0; b < B; b++) {
+                const auto& v = seg_of(k, dig, b);
+                cur[(size_t)k * B + b] = allidx.size() - (dig ? vseg.back().first + vseg.back().second : 0);
+                allidx.insert(allidx.end(), v.begin(), v.end());
+            }
+            seg.back().second = allidx.size() - seg.back().first;
+        }
+    size_t nvals = dseg.front().first;
     size_t ndig = allidx.size() - nvals;
-    const size_t nent = open_ent.size(), nopen = nent * 2 * LB;
-    allidx.insert(allidx.end(), open_ent.begin(), open_ent.end());
+    size_t nent = 0;
+    std::vector<int64_t> ent0(B);
+    for (int b = 0; b < B; b++) {
+        ent0[b] = (int64_t)nent;
+        allidx.insert(allidx.end(), lay[b].oent.begin(), lay[b].oent.end());
+        nent += lay[b].oent.size();
+    }
+    const size_t nopen = nent * 2 * LB;
     c->gidx.ensure(allidx.size());
     c->gval.ensure(nvals);
     c->gdig.ensure(ndig + 2 * nopen);
@@ -951,45 +970,39 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     ht.mark("sync_gather");
     auto t_s0 = std::chrono::steady_clock::now();
 
-    // ---- 8. StarkProof::to_bytes (DESIGN.md "Proof format")
+    // ---- 8. StarkProof::to_bytes (DESIGN.md "Proof format"), one proof per pool task
     const Digest* open_t = gd + ndig;
     const Digest* open_h = gd + ndig + nopen;
-    size_t cur_lde = 0, cur_h = vidx_lde.size(), cur_t = 0, cur_hd = didx_t.size();
-    std::vector<size_t> cur_fv(nl), cur_fd(nl);
-    {
-        size_t off = vidx_lde.size() + vidx_h.size();
-        for (unsigned l = 0; l < nl; l++) { cur_fv[l] = off; off += vidx_f[l].size(); }
-        off = didx_t.size() + didx_h.size();
-        for (unsigned l = 0; l < nl; l++) { cur_fd[l] = off; off += didx_f[l].size(); }
-    }
-    auto write_paths = [&](BW& w, const BatchOpening& op, size_t& cursor) {
-        size_t slot = w.len_slot();
-        w.u8(op.size());
-        for (size_t i = 0; i < op.size(); i++) {
-            w.u8(op.len[i]);
-            w.put(&gd[cursor], 32 * op.len[i]);
-            cursor += op.len[i];
-        }
-        w.len_patch(slot);
-    };
-    auto write_lde_paths = [&](BW& w, const Layout& L, size_t& cursor, const Digest* open) {
-        size_t slot = w.len_slot();
-        w.u8(L.op.size());
-        size_t r = 0;
-        for (size_t i = 0; i < L.op.size(); i++) {
-            w.u8(L.op.len[i]);
-            uint8_t* q = w.at(32 * L.op.len[i]);
-            for (size_t k = 0; k < L.op.len[i]; k++, r++) {
-                int64_t ref = L.ref[r];
-                memcpy(q + 32 * k, (ref >= 0 ? gd[cursor++] : open[-ref - 1]).w, 32);
-            }
-        }
-        w.len_patch(slot);
-    };
-    for (int b = 0; b < B; b++) {
+    pool.parallel_for(B, [&](int b) {
         auto& j = jobs[b];
+        const Layout& Lb = lay[b];
+        const size_t eoff = (size_t)ent0[b] * 2 * LB;  // this proof's first recomputed-subtree slot
+        auto write_paths = [&](BW& w, const BatchOpening& op, size_t cursor) {
+            size_t slot = w.len_slot();
+            w.u8(op.size());
+            for (size_t i = 0; i < op.size(); i++) {
+                w.u8(op.len[i]);
+                w.put(&gd[cursor], 32 * op.len[i]);
+                cursor += op.len[i];
+            }
+            w.len_patch(slot);
+        };
+        auto write_lde_paths = [&](BW& w, size_t cursor, const Digest* open) {
+            size_t slot = w.len_slot();
+            w.u8(Lb.op.size());
+            size_t r = 0;
+            for (size_t i = 0; i < Lb.op.size(); i++) {
+                w.u8(Lb.op.len[i]);
+                uint8_t* q = w.at(32 * Lb.op.len[i]);
+                for (size_t k = 0; k < Lb.op.len[i]; k++, r++) {
+                    int64_t ref = Lb.ref[r];
+                    memcpy(q + 32 * k, (ref >= 0 ? gd[cursor++] : open[(size_t)(-ref - 1) + eoff]).w, 32);
+                }
+            }
+            w.len_patch(slot);
+        };
         const u64 nu = j.pos.size();
-        BW w(c->hs.ser);
+        BW w(j.bytes);
         w.reserve(j.commitments.size() + nu * 8 * (7 + DE + 8 * DE * nl) + (2 + nl) * nu * 32 * ilog2(N) +
                    rem_len * 8 * DE + 1024);
         // Context
@@ -1002,14 +1015,12 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         // trace queries
         w.u8(1);
         w.u32(nu * 7 * 8);
-        w.u64s(&gv[cur_lde], nu * 7);
-        cur_lde += nu * 7;
-        write_lde_paths(w, lay[b], cur_t, open_t);
+        w.u64s(&gv[vcur[b]], nu * 7);
+        write_lde_paths(w, dcur[b], open_t);
         // constraint queries
         w.u32(nu * 8 * DE);
-        w.u64s(&gv[cur_h], nu * DE);
-        cur_h += nu * DE;
-        write_lde_paths(w, lay[b], cur_hd, open_h);
+        w.u64s(&gv[vcur[(size_t)B + b]], nu * DE);
+        write_lde_paths(w, dcur[(size_t)B + b], open_h);
         // OOD frame (E elements)
         w.u16(1 + 14 * 8 * DE);
         w.u8(2);
@@ -1019,18 +1030,17 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         // FRI proof
         w.u8(nl);
         for (unsigned l = 0; l < nl; l++) {
-            u64 nk = lay[b].fpos[l].size();
+            u64 nk = Lb.fpos[l].size();
             w.u32(nk * 8 * 8 * DE);
-            w.u64s(&gv[cur_fv[l]], nk * 8 * DE);
-            cur_fv[l] += nk * 8 * DE;
-            write_paths(w, lay[b].fops[l], cur_fd[l]);
+            w.u64s(&gv[vcur[(size_t)(2 + l) * B + b]], nk * 8 * DE);
+            write_paths(w, Lb.fops[l], dcur[(size_t)(2 + l) * B + b]);
         }
         w.u16(rem_len * 8 * DE);
         w.u64s(j.rem.data(), rem_len * DE);
         w.u8(0);
         w.u64_(j.nonce);
-        w.finish(j.bytes);
-    }
+        w.trim();
+    });
     ht.mark("serialize");
     ht.dump(B);
     if (probe) {  // the stream has passed both events (root / query fetches synchronised it)
@@ -1128,15 +1138,16 @@ static int split_min() {
 }
 
 static void copy_unit(Batch* b, int b0, int b1) {
-    for (int k = b0; k < b1; k++) {
+    host_pool().parallel_for(b1 - b0, [&](int i0) {
+        const int k = b0 + i0;
         ProofJob& j = b->jobs[k];
         if (j.status) {
             b->st[k] = j.status;
-            continue;
+            return;
         }
         if (b->which.empty()) {  // warm-up batch (xfg_prepare): bytes discarded
             std::vector<uint8_t>().swap(j.bytes);
-            continue;
+            return;
         }
         uint32_t i = b->which[k];
         size_t need = j.bytes.size();
@@ -1151,7 +1162,7 @@ static void copy_unit(Batch* b, int b0, int b1) {
         }
         b->out_lens[i] = need;
         std::vector<uint8_t>().swap(j.bytes);
-    }
+    });
 }
 
 static void worker_main(xfg_ctx* c, int l) {
