@@ -1867,14 +1867,10 @@ int xfg_verify_batch_gpu(xfg_ctx* c, uint32_t count, const uint8_t* const* proof
         if (V.frag.size() < count) V.frag.resize(count);
         std::vector<VState>& st = V.st;
         std::vector<std::string> err(count);
-        const unsigned nt = std::max(1u, std::min<unsigned>(std::thread::hardware_concurrency(), 16));
+        // per-proof host phases on the host pool (spawning 16 threads per phase cost more than the
+        // phases' own work at 64 proofs); a proof per task
         auto parallel = [&](const std::function<void(uint32_t)>& f) {
-            std::vector<std::thread> th;
-            for (unsigned t = 0; t < nt; t++)
-                th.emplace_back([&, t] {
-                    for (uint32_t i = t; i < count; i += nt) f(i);
-                });
-            for (auto& x : th) x.join();
+            host_pool().parallel_for((int)count, [&](int i) { f((uint32_t)i); });
         };
         // 1. transcripts (host threads)
         parallel([&](uint32_t i) {
