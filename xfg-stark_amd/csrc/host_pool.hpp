@@ -98,13 +98,15 @@ class HostPool {
     }
 };
 
-// XFG_HOST_THREADS (default 8; 0 = every loop on the calling lane worker, as before the pool)
+// XFG_HOST_THREADS (default 8; 0 = every loop on the calling lane worker, as before the pool).
+// Never destroyed: lane workers of a context the process did not close may still use it while
+// static destructors run at exit; its idle threads end with the process.
 static inline HostPool& host_pool() {
-    static HostPool pool([] {
+    static HostPool* pool = new HostPool([] {
         const char* v = getenv("XFG_HOST_THREADS");
         return std::max(0, v && *v ? atoi(v) : 8);
     }());
-    return pool;
+    return *pool;
 }
 
 }  // namespace xfg

@@ -1483,17 +1483,18 @@ int xfg_prove_batch_submit(xfg_ctx* c, uint32_t count, const xfg_burn_inputs* in
     return guarded(c, [&]() -> int {
         HIPCHK(hipSetDevice(c->device));
         std::unique_ptr<Batch> bp(new Batch());
+        // validation + marshalling (three Keccak-256 per proof) per input on the host pool: the
+        // submitting thread is the start of every batch's latency
+        std::vector<AirConst> airs(count);
+        std::vector<std::string> errs(count);
+        host_pool().parallel_for((int)count, [&](int i) { statuses[i] = marshal(&inputs[i], airs[i], errs[i]); });
         for (uint32_t i = 0; i < count; i++) {
-            AirConst a;
-            std::string err;
-            int st = marshal(&inputs[i], a, err);
-            statuses[i] = st;
-            if (st) {
-                c->err = err;
+            if (statuses[i]) {
+                c->err = errs[i];
                 continue;
             }
             bp->jobs.emplace_back();
-            bp->jobs.back().air = a;
+            bp->jobs.back().air = airs[i];
             bp->which.push_back(i);
         }
         if (outs) bp->outs.assign(outs, outs + count);
