@@ -526,7 +526,7 @@ def main():
                          # the kernel is VALU-issue-bound: the same launch set
                          # against the VALU ceiling, instruction counts from the same PMC record
                          "valu": valu_roofline(pmc, lde_ms, WIDTH * per * n * BLOWUP),
-                         "kernel": "trace LDE (ntt_pass_a_cos2 + ntt_pass_b_tq<8,8,4>), 7 columns x "
+                         "kernel": "trace LDE (ntt_pass_a_cos2 + ntt_pass_b_tq<8,8,4,split>), 7 columns x "
                                    f"{per} proofs, {lde_ms:.3f} ms/launch-set, {lde_bytes} algorithmic B",
                          # the same launch sets inside the timed pipelined steps (per XFG_UNIT-proof unit,
                          # sharing the GPU with the other lanes' kernels)

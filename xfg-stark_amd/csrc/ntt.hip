@@ -190,6 +190,50 @@ __device__ __forceinline__ void pass_dft(u64* tile, int lognseq, const u64* ltw,
     }
 }
 
+// pass_dft for two full-radix steps (one group per thread, full tiles) with the exchange between the
+// steps in 32-bit halves: the low words go through the LDS tile, then the high words through the
+// same tile, so the tile is half the size of a 64-bit one and twice as many blocks fit a CU. Costs
+// twice the LDS instructions and two more barriers per tile.
+template <int LOGS, int LOGE, bool INV, bool FIRST_SEQ_FAST, int NT, class LDG, class STG, class PF, bool TW2D_LAST = false>
+__device__ __forceinline__ void pass_dft_split(u32* tile, int lognseq, const u64* ltw, LDG ldg, STG stg, PF pf) {
+    using PL = Plan<LOGS, LOGE>;
+    static_assert(PL::NSTEP == 2 && PL::FIRST_LOGR == LOGE, "two full-radix steps");
+    constexpr int L = NT_LOG2(NT) + LOGE - LOGS;
+    constexpr int PITCH = row_pitch(1 << LOGS, LOGE, L), E = 1 << LOGE, G = (1 << LOGS) / E;
+    auto nopf = [](int, int, int, int) {};
+    u32 hi[E];
+    int sseq = 0, sbase = 0;
+    stockham<LOGS, LOGE, LOGE, INV, FIRST_SEQ_FAST, false, NT>(
+        lognseq, 1, ltw, ldg,
+        [&](int, int seq, int base, int, u64* v) {
+            u32* row = tile + seq * PITCH + phys<LOGE>(base);
+#pragma unroll
+            for (int r = 0; r < E; r++) {
+                row[r + (r >> LOGE)] = (u32)v[r];
+                hi[r] = (u32)(v[r] >> 32);
+            }
+            sseq = seq;
+            sbase = base;
+        },
+        nopf);
+    __syncthreads();
+    // this thread's group of the second step (stockham, SEQ_FAST, q = 0)
+    const int g = threadIdx.x, seq = g & ((1 << lognseq) - 1), j = g >> lognseq;
+    u32 lo[E];
+#pragma unroll
+    for (int r = 0; r < E; r++) lo[r] = tile[seq * PITCH + phys2<LOGE>(j, r * G)];
+    __syncthreads();
+    {
+        u32* row = tile + sseq * PITCH + phys<LOGE>(sbase);
+#pragma unroll
+        for (int r = 0; r < E; r++) row[r + (r >> LOGE)] = hi[r];
+    }
+    __syncthreads();
+    auto ldl = [&](int sq, int jj, int o) { return (u64)lo[o / G] | ((u64)tile[sq * PITCH + phys2<LOGE>(jj, o)] << 32); };
+    stockham<LOGS, LOGE, LOGE, INV, true, false, NT, decltype(ldl), STG, PF, TW2D_LAST>(lognseq, E, ltw, ldl, stg, pf);
+    __syncthreads();
+}
+
 __host__ __device__ u64 fourstep_main(int logn, int logbeta);
 struct NttArgs {
     const u64* in;
@@ -537,7 +581,7 @@ __global__ __launch_bounds__(1 << LOGT) void ntt_pass_b(NttArgs a) {
 // ntt_pass_b specialised to the path every tabled LDE takes (the all-coset pass A left the four-step
 // twiddles to it): one first-step group per thread, data and table loaded up front, no run-time
 // branches for the other paths
-template <int LOGC, int LOGT, int LOGE>
+template <int LOGC, int LOGT, int LOGE, bool SPLIT = false>
 __global__ __launch_bounds__(1 << LOGT) void ntt_pass_b_tq(NttArgs a) {
     constexpr int C = 1 << LOGC, RR = Plan<LOGC, LOGE>::LAST_R, NT = 1 << LOGT;
     using PLB = Plan<LOGC, LOGE>;
@@ -547,7 +591,8 @@ __global__ __launch_bounds__(1 << LOGT) void ntt_pass_b_tq(NttArgs a) {
     const int logTR = (a.logR < LOGT + LOGE - LOGC) ? a.logR : LOGT + LOGE - LOGC;
     const int TR = 1 << logTR;
     u64* tile = lds;
-    u64* ltw = lds + TR * row_pitch(C, LOGE, LOGT + LOGE - LOGC);
+    const int tw = TR * row_pitch(C, LOGE, LOGT + LOGE - LOGC);
+    u64* ltw = SPLIT ? reinterpret_cast<u64*>(reinterpret_cast<u32*>(lds) + tw) : lds + tw;
     int bx, by;
     xcd_block(a.xcd & 2, bx, by);
     const int pt = by, k10 = bx * TR;
@@ -574,7 +619,10 @@ __global__ __launch_bounds__(1 << LOGT) void ntt_pass_b_tq(NttArgs a) {
         for (int r = 0; r < RR; r++)
             buf_st(rout, (seq + ((u32)base << a.logR)) * 8, ((u32)(r * stride) << a.logR) * 8, canon(v[r]));
     };
-    pass_dft<LOGC, LOGE, false, false, NT>(tile, logTR, ltw, ldg, stg, NoPf{});
+    if constexpr (SPLIT)
+        pass_dft_split<LOGC, LOGE, false, false, NT>(reinterpret_cast<u32*>(tile), logTR, ltw, ldg, stg, NoPf{});
+    else
+        pass_dft<LOGC, LOGE, false, false, NT>(tile, logTR, ltw, ldg, stg, NoPf{});
 }
 
 // ---------------------------------------------------------------- pass B, persistent (forward, no table)
@@ -865,6 +913,10 @@ void build_fourstep(u64* out, int logn, int logbeta, const Tables& T, hipStream_
                        logbeta, logR, logC, T);
 }
 
+static int env_knob(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v && *v ? atoi(v) : dflt;
+}
 static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
     ntt_split(a.logn, a.logR, a.logC);
     const int R = 1 << a.logR, C = 1 << a.logC;
@@ -945,6 +997,11 @@ static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
         run_pass_a<true>(a.logR, ltA, eA, ga, lds_a, s, a);
         run_pass_b<true>(a.logC, ltB, eB, gb, lds_b, s, a);
     } else {
+        // pass B of the tabled LDE with the 32-bit split exchange (pass_dft_split): 19.5 instead of 37 KiB
+        // of LDS per block, 6 instead of 4 waves per SIMD at 77 VGPRs. Same box, pass B 919-942 vs
+        // 946-961 us per 64-proof launch set, bench 12,760 vs 12,699 (5 interleaved runs).
+        // XFG_NTT_SPLIT=0 disables (A/B knob). (Pass A split: 4 waves still, VGPR-bound; neutral.)
+        static const bool split_b = env_knob("XFG_NTT_SPLIT", 1) != 0;
         // all cosets of a column tile in one block (ntt_pass_a_cos); XFG_NTT_COS=0 disables
         static const bool cos_on = [] {
             const char* v = getenv("XFG_NTT_COS");
@@ -957,7 +1014,8 @@ static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
         }();
         if (cos_on && cos2_on && a.t4 && a.logR == 8 && ltA == 8 && eA == 4 && !(a.xcd & 1) && a.logbeta >= 2) {
             a.tq_b = 1;
-            hipLaunchKernelGGL(ntt_pass_a_cos2, dim3(C >> logTC, npoly), dim3(256), lds_a, s, a);
+            static const size_t pad_a = (size_t)std::max(0, env_knob("XFG_NTT_APAD", 0));  // occupancy probe
+            hipLaunchKernelGGL(ntt_pass_a_cos2, dim3(C >> logTC, npoly), dim3(256), lds_a + pad_a, s, a);
         } else if (cos_on && a.t4 && a.logR == 8 && ltA == 8 && eA == 4 && !(a.xcd & 1)) {
             a.tq_b = 1;
             hipLaunchKernelGGL(ntt_pass_a_cos<8>, dim3(C >> logTC, npoly), dim3(256), lds_a, s, a);
@@ -990,7 +1048,12 @@ static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
             hipLaunchKernelGGL((ntt_pass_b_pers<10, 8, 5, 0, 2>), dim3(nb), dim3(256), lds_b, s, a, ntx, ntiles);
         } else if (!bpers16 && tqspec_on && eB == 4 && ltB == 8 && a.logC == 8 && a.logR >= 4 && a.t4 && a.tq_b && a.pt &&
                    !a.yblk) {
-            hipLaunchKernelGGL((ntt_pass_b_tq<8, 8, 4>), gb, dim3(256), lds_b, s, a);  // lds_b < 64 KiB here
+            static const size_t pad_b = (size_t)std::max(0, env_knob("XFG_NTT_BPAD", 0));  // occupancy probe
+            if (split_b) {
+                const size_t l = ((size_t)(1 << logTR) * row_pitch(C, 4, 4) * 4 + C * 8);
+                hipLaunchKernelGGL((ntt_pass_b_tq<8, 8, 4, true>), gb, dim3(256), l + pad_b, s, a);
+            } else
+                hipLaunchKernelGGL((ntt_pass_b_tq<8, 8, 4>), gb, dim3(256), lds_b + pad_b, s, a);  // lds_b < 64 KiB here
         } else if (bpers16 && eB == 4 && ltB == 8 && a.logC == 8 && a.logR >= 4 && a.t4 && a.tq_b && a.pt) {
             const int ntx = R >> logTR, ntiles = ntx * npoly * ncos;
             if (bpers16 == 2) {
