@@ -79,7 +79,7 @@ def pmc(prefix, count, n, blowup):
     return d
 
 
-for prefix, name, shape in (("pmc", "lde_pmc.json", (64, 65536, 8)), ("c5pmc", "lde_pmc_c5.json", (1, 1 << 20, 16))):
+for prefix, name, shape in (("pmc", "lde_pmc.json", (64, 65536, 8)), ("c5pmc", "lde_pmc_c5.json", (4, 1 << 20, 16))):
     d = pmc(prefix, *shape)
     if d:
         res[name] = d
