@@ -25,7 +25,9 @@
  * ("Proof format"); the caller owns all host buffers, the library owns device memory (pooled per
  * context). `out == NULL` (or *out_len too small) returns the required size in *out_len.
  * A context is bound to one HIP device; it owns XFG_LANES (default 7) lanes, each a HIP stream with
- * its workspace and a host worker thread. Submit from one thread per context.
+ * its workspace and a host worker thread; the per-proof host work of the lanes (transcript replay,
+ * opening plans, serialisation) runs on a process-wide pool of XFG_HOST_THREADS (default 8) threads.
+ * Submit from one thread per context.
  */
 #ifndef XFG_STARK_H
 #define XFG_STARK_H
