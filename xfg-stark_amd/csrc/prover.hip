@@ -879,7 +879,8 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     });
     ht.mark("queries_plan");
     // one index buffer, one value buffer, one digest buffer; segment per source, the proofs' lists
-    // end to end inside each segment. cur_*[b]: where proof b's values / digests of a segment start
+    // end to end inside each segment. vcur / dcur[k * B + b]: where proof b's values / digests of segment k
+    // start in the host copies gv / gd
     auto& allidx = c->hs.allidx;
     allidx.clear();
     const int NS = 2 + (int)nl;  // value segments: trace LDE, composition LDE, FRI layers (same count of digest segments)
