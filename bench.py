@@ -168,23 +168,47 @@ def pipelined_steps(submit_fn, collect_fn, batches, rank, world, per_rank, devic
     pending, out = [], None
     tl = [] if os.environ.get("XFG_BENCH_TIMELINE") else None  # step completion times (stderr)
     ts = []
-    t0 = time.perf_counter()
+    # XFG_BENCH_PHASES=1: host time of the loop's phases (scatter, submit, wait, gather), stderr
+    ph = {"scatter": 0.0, "submit": 0.0, "wait": 0.0, "gather": 0.0} if os.environ.get("XFG_BENCH_PHASES") else None
+    clk = time.perf_counter
+
+    def collect_gather(p):
+        t1 = clk()
+        got = collect_fn(p)
+        if ph is not None and hasattr(p, "wait"):
+            p.wait()
+        t2 = clk()
+        r = gather_proofs(got, rank, world, per_rank, device, dist)
+        if ph is not None:
+            ph["wait"] += t2 - t1
+            ph["gather"] += clk() - t2
+        return r
+
+    t0 = clk()
     for i, b in enumerate(batches):
+        t1 = clk()
         local = scatter_inputs(b, rank, world, per_rank, device, dist, packed[i] if packed else None)
+        t2 = clk()
         pending.append(submit_fn(local))
+        if ph is not None:
+            ph["scatter"] += t2 - t1
+            ph["submit"] += clk() - t2
         if tl is not None:
-            ts.append(time.perf_counter() - t0)
+            ts.append(clk() - t0)
         if len(pending) >= depth:
-            out = gather_proofs(collect_fn(pending.pop(0)), rank, world, per_rank, device, dist)
+            out = collect_gather(pending.pop(0))
             if tl is not None:
-                tl.append(time.perf_counter() - t0)
+                tl.append(clk() - t0)
     while pending:
-        out = gather_proofs(collect_fn(pending.pop(0)), rank, world, per_rank, device, dist)
+        out = collect_gather(pending.pop(0))
         if tl is not None:
-            tl.append(time.perf_counter() - t0)
+            tl.append(clk() - t0)
     if tl:
         print("timeline ms: " + " ".join(f"{t * 1e3:.1f}" for t in tl), file=sys.stderr)
         print("submitted ms: " + " ".join(f"{t * 1e3:.1f}" for t in ts), file=sys.stderr)
+    if ph is not None:
+        print("phases ms: " + " ".join(f"{k}={v * 1e3:.1f}" for k, v in ph.items()) +
+              f" total={(clk() - t0) * 1e3:.1f}", file=sys.stderr)
     return out
 
 

@@ -350,9 +350,15 @@ class PendingBatch:
         self._outs, self._lens, self._sts = outs, lens, sts
         self._res = None
 
+    def wait(self):
+        """block until every proof of the batch is done (idempotent); the batch's status code"""
+        if not hasattr(self, "_wst"):
+            self._wst = _lib.xfg_batch_wait(self._p._ctx, self._t)
+        return self._wst
+
     def result(self):
         if self._res is None:
-            st = _lib.xfg_batch_wait(self._p._ctx, self._t)
+            st = self.wait()
             if st:
                 self._p._free.append(self._buf)
                 raise self._p._err(st)
@@ -373,7 +379,7 @@ class PendingBatch:
         objects. Returns the record size. Any per-proof error raises."""
         import numpy as np
         if self._res is None:
-            st = _lib.xfg_batch_wait(self._p._ctx, self._t)
+            st = self.wait()
             if st:
                 self._p._free.append(self._buf)
                 self._res = []
