@@ -59,131 +59,186 @@ def unpack_inputs(arr):
     return res
 
 
-def scatter_all(batches, rank, world, per_rank, device, dist, packed=None):
-    """every step's shard in ONE scatter (rank 0 holds all steps' inputs in HBM): [K, per_rank, REC]
-    uint8 records of this rank on the host, unpacked per step by the caller. One collective per
-    window instead of one per step -- a per-step scatter and the host sync on its shard waited
-    ~0.8 ms per step for its RCCL kernel on a GPU the prover's lanes keep full"""
-    import torch
-    K = len(batches)
-    if rank == 0:
-        if packed is None:
-            packed = [torch.from_numpy(pack_inputs(b)).to(device).view(world, per_rank, REC) for b in batches]
-        big = torch.stack(list(packed[:K]), dim=1)  # [world, K, per_rank, REC]
-        chunks = list(big.unbind(0))
-    else:
-        chunks = None
-    local = torch.empty((K, per_rank, REC), dtype=torch.uint8, device=device)
-    dist.scatter(local, chunks, src=0)
-    return local.cpu().numpy()
-
-
-def scatter_inputs(all_inputs, rank, world, per_rank, device, dist, packed=None):
-    """rank 0's batch inputs -> this rank's shard (list of prove kwargs). `packed` = the batch
-    already packed into a [world, per_rank, REC] uint8 device tensor on rank 0 (resident in HBM)."""
-    import torch
-    if dist is None:
-        return all_inputs
-    if rank == 0:
-        if packed is None:
-            packed = torch.from_numpy(pack_inputs(all_inputs)).to(device).view(world, per_rank, REC)
-        chunks = list(packed.unbind(0))
-    else:
-        chunks = None
-    local = torch.empty((per_rank, REC), dtype=torch.uint8, device=device)
-    dist.scatter(local, chunks, src=0)
-    return unpack_inputs(local.cpu().numpy())
-
-
-class _Exchange:
-    """reused buffers of gather_proofs: a pinned host record per rank (double-buffered, so a record
-    is never rewritten while its host-to-device copy may still run), rank 0's device gather buffer
-    and its pinned host copy"""
-    send = None
-    flip = 0
-    big = None
-    host = None
-
-
 def _pinned(nbytes, device):
     import torch
     return torch.empty(nbytes, dtype=torch.uint8, pin_memory=device.type == "cuda")
 
 
-def gather_proofs(proofs, rank, world, per_rank, device, dist):
-    """this rank's proofs -> all proofs on rank 0 (None elsewhere) over the process group: one gather
-    of [per_rank int64 lengths | concatenated proofs], padded to the longest rank record.
-    `proofs` is a list of proof bytes or a submitted batch (xfgstark.PendingBatch), whose proofs
-    are packed straight from the workers' output buffer into a pinned record. Rank 0 gathers into
-    one reused device buffer, copies it to pinned host memory in one D2H and returns zero-copy
-    memoryviews into it (valid until the next call)."""
-    import numpy as np
-    import torch
-    if dist is None:
-        return proofs
-    X = _Exchange
-    hdr = 8 * per_rank
-    if hasattr(proofs, "packed_into"):
-        cap = hdr + per_rank * proofs._cap
-    else:
-        cap = hdr + sum(len(p) for p in proofs)
-    if X.send is None or X.send[0].numel() < cap:
-        X.send = [_pinned(cap + (1 << 20), device), _pinned(cap + (1 << 20), device)]
-    X.flip ^= 1
-    rec = X.send[X.flip]
-    buf = rec.numpy()
-    if hasattr(proofs, "packed_into"):
-        mine = proofs.packed_into(buf)
-    else:
-        lens = np.array([len(p) for p in proofs], dtype=np.int64)
-        buf[:hdr] = lens.view(np.uint8)
-        off = hdr
-        for p in proofs:  # one copy of each proof, straight into the record
-            buf[off:off + len(p)] = np.frombuffer(p, dtype=np.uint8)
-            off += len(p)
-        mine = off
-    size = torch.tensor([mine], dtype=torch.int64, device=device)
-    dist.all_reduce(size, op=dist.ReduceOp.MAX)
-    size = int(size.item())
-    t = rec[:size].to(device, non_blocking=True) if device.type == "cuda" else rec[:size]
-    got = None
-    if rank == 0:
-        if X.big is None or X.big.shape[0] != world or X.big.shape[1] < size:
-            X.big = torch.empty((world, size + (1 << 20)), dtype=torch.uint8, device=device)
-        got = [X.big[r, :size] for r in range(world)]
-    dist.gather(t, got, dst=0)
-    if rank != 0:
-        return None
-    if device.type == "cuda":  # one D2H of all ranks' records into a reused pinned buffer
-        if X.host is None or X.host.numel() < world * size:
-            X.host = _pinned(world * size + (8 << 20), device)
-        host = X.host[:world * size].view(world, size)
-        host.copy_(X.big[:, :size])
-        allb = host.numpy()
-    else:
-        allb = X.big[:, :size].numpy()
-    out = []
-    for r in range(world):
-        row = allb[r]
-        mv, off = memoryview(row), hdr
-        for ln in row[:hdr].view(np.int64):
-            out.append(mv[off:off + int(ln)])
-            off += int(ln)
-    return out
+class Exchange:
+    """The exchange step of a sharded run (BASELINE configs[3]: 512 proofs over 8 GPUs; the reference's
+    batch pattern is src/burn_mint_verifier.rs:326-338): rank 0 scatters each step's packed inputs,
+    every rank proves its shard, rank 0 gathers the proofs. Nothing here makes the host wait on the
+    GPU inside a step:
+
+    * inputs -- one scatter per step, issued `lookahead` steps before the step is submitted
+      (asynchronous collective on a side stream, a non-blocking D2H of the shard into pinned memory,
+      an event); the submission syncs that event, long complete by then;
+    * proofs -- every rank's batch is proven straight into a fixed-size pinned record (int64 lengths,
+      then one xfg_proof_size_bound slot per proof: no packing copy, no size all-reduce). Once the
+      batch is done the record goes H2D into an asynchronous gather to rank 0, which copies the
+      gathered records D2H into a pinned ring slot, all on the side stream, with an event at the
+      end; the host awaits it only when the slot comes round again or when the proofs are read.
+
+    On the gloo backend (CPU rehearsal, tests/test_dist.py) the same steps run on host tensors and
+    the collectives' Work handles stand in for the events."""
+
+    def __init__(self, rank, world, per, cap, device, dist, send_slots, recv_slots=3, lookahead=4):
+        import torch
+        self.rank, self.world, self.per, self.cap = rank, world, per, cap
+        self.device, self.dist, self.cuda = device, dist, device.type == "cuda"
+        self.hdr = 8 * per
+        self.rec = self.hdr + per * cap
+        self.stream = torch.cuda.Stream(device) if self.cuda else None
+        self.send = [_pinned(self.rec, device) for _ in range(send_slots)]
+        self.send_dev = [torch.empty(self.rec, dtype=torch.uint8, device=device)
+                         for _ in range(send_slots)] if self.cuda else None
+        self.send_busy = [None] * send_slots  # completion handle of the gather that last read the slot
+        self.send_owned = [False] * send_slots  # claimed by a batch that has not been gathered yet
+        self.next_send = 0
+        self.recv_busy = [None] * recv_slots
+        self.next_recv = 0
+        if rank == 0:
+            self.recv_host = [_pinned(world * self.rec, device).view(world, self.rec) for _ in range(recv_slots)]
+            self.recv_dev = [torch.empty((world, self.rec), dtype=torch.uint8, device=device)
+                             for _ in range(recv_slots)] if self.cuda else None
+        self.lookahead = max(1, lookahead)
+        ring = self.lookahead + 1
+        self.in_host = [_pinned(per * REC, device).view(per, REC) for _ in range(ring)]
+        self.in_dev = [torch.empty((per, REC), dtype=torch.uint8, device=device) for _ in range(ring)] \
+            if self.cuda else None
+        self.in_pending = [None] * ring
+        self.packed, self.nsteps = None, 0
+
+    def _done(self, h):
+        if h is None:
+            return
+        if self.cuda:
+            h.synchronize()  # torch.cuda.Event at the end of the side stream's work
+        else:
+            h.wait()  # the collective's Work (gloo)
+
+    def _side(self):
+        import contextlib
+        import torch
+        return torch.cuda.stream(self.stream) if self.cuda else contextlib.nullcontext()
+
+    def _event(self):
+        import torch
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        return ev
+
+    # ---- inputs
+    def start_inputs(self, packed, nsteps):
+        """`packed`: rank 0's list of [world, per, REC] uint8 tensors, one per step (resident in HBM
+        before the timed region), None elsewhere. Issues the first `lookahead` scatters."""
+        self.packed, self.nsteps = packed, nsteps
+        for i in range(min(self.lookahead, nsteps)):
+            self._scatter(i)
+
+    def _scatter(self, i):
+        slot = i % len(self.in_pending)
+        chunks = list(self.packed[i].unbind(0)) if self.rank == 0 else None
+        if self.cuda:
+            with self._side():
+                w = self.dist.scatter(self.in_dev[slot], chunks, src=0, async_op=True)
+                w.wait()  # the side stream waits for the collective; the host does not
+                self.in_host[slot].copy_(self.in_dev[slot], non_blocking=True)
+                h = self._event()
+        else:
+            h = self.dist.scatter(self.in_host[slot], chunks, src=0, async_op=True)
+        self.in_pending[slot] = (i, h)
+
+    def inputs(self, i):
+        """step i's shard as prove kwargs (issues step i + lookahead's scatter)"""
+        slot = i % len(self.in_pending)
+        j, h = self.in_pending[slot]
+        assert j == i, (j, i)
+        self._done(h)
+        kws = unpack_inputs(self.in_host[slot].numpy())
+        self.in_pending[slot] = None
+        if i + self.lookahead < self.nsteps:
+            self._scatter(i + self.lookahead)
+        return kws
+
+    # ---- proofs
+    def claim(self):
+        """a free send record for the next batch: (slot, host address, bytes)"""
+        s = self.next_send
+        if self.send_owned[s]:
+            raise RuntimeError("Exchange: more batches in flight than send records")
+        self.next_send = (s + 1) % len(self.send)
+        self._done(self.send_busy[s])
+        self.send_busy[s] = None
+        self.send_owned[s] = True
+        return s, self.send[s].data_ptr(), self.rec
+
+    def gather(self, s):
+        """record s holds a complete batch: send it to rank 0 (asynchronous); returns a Gathered"""
+        r = None
+        with self._side():
+            if self.rank == 0:
+                r = self.next_recv
+                self.next_recv = (r + 1) % len(self.recv_busy)
+                self._done(self.recv_busy[r])
+            if self.cuda:
+                self.send_dev[s].copy_(self.send[s], non_blocking=True)
+                got = list(self.recv_dev[r].unbind(0)) if self.rank == 0 else None
+                w = self.dist.gather(self.send_dev[s], got, dst=0, async_op=True)
+                w.wait()
+                if self.rank == 0:
+                    self.recv_host[r].copy_(self.recv_dev[r], non_blocking=True)
+                h = self._event()
+            else:
+                got = list(self.recv_host[r].unbind(0)) if self.rank == 0 else None
+                h = self.dist.gather(self.send[s], got, dst=0, async_op=True)
+        self.send_busy[s] = h
+        self.send_owned[s] = False
+        if r is not None:
+            self.recv_busy[r] = h
+        return Gathered(self, h, r)
+
+    def drain(self):
+        for h in self.send_busy + self.recv_busy:
+            self._done(h)
 
 
-def sharded_step(prove_fn, all_inputs, rank, world, per_rank, device, dist):
-    """scatter packed inputs from rank 0, prove the local shard, gather proof bytes to rank 0.
-    Returns the list of proofs (bytes) on rank 0, None elsewhere."""
-    local = scatter_inputs(all_inputs, rank, world, per_rank, device, dist)
-    return gather_proofs(prove_fn(local), rank, world, per_rank, device, dist)
+class Gathered:
+    """one step's gathered proofs on rank 0 (a handle on the asynchronous exchange)"""
+
+    def __init__(self, ex, h, slot):
+        self.ex, self.h, self.slot = ex, h, slot
+
+    def proofs(self):
+        """waits for the exchange; rank 0: all ranks' proofs in rank order, zero-copy memoryviews
+        into the pinned ring slot (valid until the slot is reused, recv_slots gathers later); None
+        elsewhere. A zero or oversized length (a failed proof) raises."""
+        import numpy as np
+        ex = self.ex
+        ex._done(self.h)
+        if self.slot is None:
+            return None
+        allb = ex.recv_host[self.slot].numpy()
+        out = []
+        for q in range(ex.world):
+            row = allb[q]
+            mv = memoryview(row)
+            for i, ln in enumerate(row[:ex.hdr].view(np.int64)):
+                if not 0 < ln <= ex.cap:
+                    raise RuntimeError(f"exchange: rank {q} proof {i} has no proof in its record (length {ln})")
+                off = ex.hdr + i * ex.cap
+                out.append(mv[off:off + int(ln)])
+        return out
 
 
-def pipelined_steps(submit_fn, collect_fn, batches, rank, world, per_rank, device, dist, packed=None, depth=2):
-    """run len(batches) steps with `depth` batches in flight: every step's shard is scattered at the
-    start (one collective), step i+depth-1 is submitted before step i's proofs are collected and
-    gathered, so the host tail of one batch (and the Python collection) overlaps the kernels of the
-    next ones. Every step is proven in full; returns the last step's proofs on rank 0."""
+def pipelined_steps(submit_fn, collect_fn, batches, depth=2, ex=None, packed=None):
+    """run len(batches) steps with `depth` batches in flight: step i+depth-1 is submitted before step
+    i's proofs are collected, so the host tail of one batch (and the collection) overlaps the kernels
+    of the next ones. Every step is proven in full. Single process (ex None): submit_fn(kws) ->
+    pending, collect_fn(pending) -> proofs; returns the last step's proofs. Sharded (ex an Exchange):
+    each step's shard comes from its own scatter, submit_fn(kws, record) proves into an exchange
+    record and the completed record is gathered to rank 0; returns the last step's proofs on rank 0,
+    None elsewhere, after every exchange of the window has completed."""
     pending, out = [], None
     tl = [] if os.environ.get("XFG_BENCH_TIMELINE") else None  # step completion times (stderr)
     ts = []
@@ -191,38 +246,54 @@ def pipelined_steps(submit_fn, collect_fn, batches, rank, world, per_rank, devic
     ph = {"scatter": 0.0, "submit": 0.0, "wait": 0.0, "gather": 0.0} if os.environ.get("XFG_BENCH_PHASES") else None
     clk = time.perf_counter
 
-    def collect_gather(p):
+    def collect(item):
+        p, s = item
         t1 = clk()
-        got = collect_fn(p)
-        if ph is not None and hasattr(p, "wait"):
-            p.wait()
-        t2 = clk()
-        r = gather_proofs(got, rank, world, per_rank, device, dist)
+        if ex is None:
+            got = collect_fn(p)
+            if ph is not None and hasattr(p, "wait"):
+                p.wait()
+            t2 = clk()
+        else:
+            p.record_ready()  # the batch is complete in its record (raises on a failed proof)
+            t2 = clk()
+            got = ex.gather(s)
         if ph is not None:
             ph["wait"] += t2 - t1
             ph["gather"] += clk() - t2
-        return r
+        return got
 
     t0 = clk()
-    shards = scatter_all(batches, rank, world, per_rank, device, dist, packed) if (dist is not None and batches) else None
+    if ex is not None:
+        ex.start_inputs(packed, len(batches))
     for i, b in enumerate(batches):
         t1 = clk()
-        local = unpack_inputs(shards[i]) if shards is not None else b
+        s, rec = None, None
+        if ex is not None:
+            b = ex.inputs(i)
+            s, addr, nbytes = ex.claim()
+            rec = (addr, nbytes)
         t2 = clk()
-        pending.append(submit_fn(local))
+        pending.append((submit_fn(b) if rec is None else submit_fn(b, rec), s))
         if ph is not None:
             ph["scatter"] += t2 - t1
             ph["submit"] += clk() - t2
         if tl is not None:
             ts.append(clk() - t0)
         if len(pending) >= depth:
-            out = collect_gather(pending.pop(0))
+            out = collect(pending.pop(0))
             if tl is not None:
                 tl.append(clk() - t0)
     while pending:
-        out = collect_gather(pending.pop(0))
+        out = collect(pending.pop(0))
         if tl is not None:
             tl.append(clk() - t0)
+    if ex is not None:
+        t1 = clk()
+        out = out.proofs() if out is not None else None
+        ex.drain()
+        if ph is not None:
+            ph["gather"] += clk() - t1
     if tl:
         print("timeline ms: " + " ".join(f"{t * 1e3:.1f}" for t in tl), file=sys.stderr)
         print("submitted ms: " + " ".join(f"{t * 1e3:.1f}" for t in ts), file=sys.stderr)
@@ -465,24 +536,27 @@ def main():
     per = args.per_gpu
     # workspace allocation, code-object load and one host output buffer per batch in flight (setup,
     # not a proving step)
-    prover.prepare(per, n, buffers=args.depth)
+    prover.prepare(per, n, buffers=0 if dist is not None else args.depth)
 
     # synthetic inputs for every step, generated before the timed region (rank 0 holds the
-    # batches; for N > 1 they are packed into HBM and scattered over RCCL inside each step)
+    # batches; for N > 1 they are packed into HBM and each step's shard is scattered over RCCL)
     total_steps = args.warmup + args.steps
     batches = [[synthetic.burn_inputs(k * per * world + i) for i in range(per * world)] if rank == 0 else None
                for k in range(total_steps)]
-    packed = None
+    packed, ex = None, None
     if dist is not None:
         packed = [torch.from_numpy(pack_inputs(b)).to(device).view(world, per, REC) if rank == 0 else None
                   for b in batches]
+        # the exchange's pinned records and device buffers (setup): one send record per batch in
+        # flight plus the ones whose gathers may still run
+        ex = Exchange(rank, world, per, prover.proof_size_bound(n), device, dist, send_slots=args.depth + 3)
 
-    def submit_fn(kws):
+    def submit_fn(kws, record=None):
+        if record is not None:  # sharded: proofs written straight into the exchange record
+            return prover.submit_batch_record(kws, n, *record)
         return prover.submit_batch(kws, trace_length=n)
 
     def collect_fn(pending):
-        if dist is not None:  # packed straight into the exchange record by gather_proofs
-            return pending
         res = pending.result()
         for r in res:
             if isinstance(r, Exception):
@@ -495,13 +569,13 @@ def main():
         torch.cuda.synchronize(gpu)
 
     if args.warmup:
-        pipelined_steps(submit_fn, collect_fn, batches[:args.warmup], rank, world, per, device, dist,
-                        packed[:args.warmup] if packed else None, args.depth)
+        pipelined_steps(submit_fn, collect_fn, batches[:args.warmup], args.depth, ex,
+                        packed[:args.warmup] if packed else None)
     barrier()
     prover.lde_probe(True)  # HIP events around every trace-LDE launch set inside the timed steps
     t0 = time.perf_counter()
-    out = pipelined_steps(submit_fn, collect_fn, batches[args.warmup:], rank, world, per, device, dist,
-                          packed[args.warmup:] if packed else None, args.depth)
+    out = pipelined_steps(submit_fn, collect_fn, batches[args.warmup:], args.depth, ex,
+                          packed[args.warmup:] if packed else None)
     barrier()
     el = time.perf_counter() - t0
     el_t = torch.tensor([el], dtype=torch.float64, device=device)
@@ -526,10 +600,15 @@ def main():
             want = [p.to_bytes() for p in prover.prove_batch(batches[-1], trace_length=n)]
             assert last == want, "gathered proofs differ from a direct prove_batch"
 
+    if rank != 0:  # the side measurements below are rank 0's
+        prover.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        return
+
     # one synchronous batch call (no pipelining), for reference
     t = time.perf_counter()
-    prover.prove_batch(batches[-1][:per] if rank == 0 else [synthetic.burn_inputs(i) for i in range(per)],
-                       trace_length=n)
+    prover.prove_batch(batches[-1][:per], trace_length=n)
     sync_call_ms = (time.perf_counter() - t) * 1e3
 
     # ---- roofline: trace LDE kernel pair, algorithmic bytes 8*w*(n+N) per proof
@@ -539,60 +618,64 @@ def main():
     pmc, traffic_src = pmc_record(per, n, BLOWUP)
     traffic = pmc["traffic_bytes"] if pmc else None
     prover.set_timing(True)
-    prover_stage = {}
-    if rank == 0:
-        prover.prove_batch([synthetic.burn_inputs(i) for i in range(per)], trace_length=n)
-        prover_stage = {k: round(v, 3) for k, v in prover.stage_times().items()}
+    prover.prove_batch([synthetic.burn_inputs(i) for i in range(per)], trace_length=n)
+    prover_stage = {k: round(v, 3) for k, v in prover.stage_times().items()}
     prover.set_timing(False)
-    vrate = verify_rate(prover, last[:per], batches[-1][:per]) if rank == 0 else None
-    c5 = None if (args.no_config5 or rank != 0) else config5(prover, gpu)
+    vrate = verify_rate(prover, last[:per], batches[-1][:per])
+    c5 = None if args.no_config5 else config5(prover, gpu)
 
-    if rank == 0:
-        total = per * world * args.steps
-        line = {
-            "metric": "burn-proofs/sec (2^16-step trace, blowup=8)",
-            "value": total / el,
-            "unit": "proofs/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": el / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u64",
-            "data": "synthetic",
-            "config": {
-                "workload": f"batch of {per} burn proofs per GPU (configs[2]; configs[3] = 512 proofs on 8 GPUs)",
-                "trace_length": n, "blowup": BLOWUP, "proof_options": "42/8/4/None/8/31",
-                "proofs_per_step": per * world,
-                "parallelism": f"dp{world} (independent proofs; RCCL scatter of inputs, gather of proof bytes)",
-                "submission": f"pipelined, depth {args.depth} (xfg_prove_batch_submit / xfg_batch_wait)",
-            },
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
-                         "traffic_source": traffic_src,
-                         # the kernel is VALU-issue-bound: the same launch set
-                         # against the VALU ceiling, instruction counts from the same PMC record
-                         "valu": valu_roofline(pmc, lde_ms, WIDTH * per * n * BLOWUP),
-                         "kernel": "trace LDE (ntt_pass_a_cos2 + ntt_pass_b_tq<8,8,4,split>), 7 columns x "
-                                   f"{per} proofs, {lde_ms:.3f} ms/launch-set, {lde_bytes} algorithmic B",
-                         # the same launch sets inside the timed pipelined steps (per XFG_UNIT-proof unit,
-                         # sharing the GPU with the other lanes' kernels)
-                         "in_pipeline": in_pipeline(pipe_ms, pipe_sets, pipe_polys, n)},
-            "whole_proof": whole_proof_line(total / el, n, world),
-            "verified": verified,
-            "verify": vrate,
-            "stage_ms_one_batch": prover_stage,
-            "sync_prove_batch_ms": round(sync_call_ms, 3),
-        }
-        if c5:
-            line["config5"] = c5
-        if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
-        print(json.dumps(line), flush=True)
+    total = per * world * args.steps
+    line = {
+        "metric": "burn-proofs/sec (2^16-step trace, blowup=8)",
+        "value": total / el,
+        "unit": "proofs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic",
+        "config": {
+            "workload": f"batch of {per} burn proofs per GPU (configs[2]; configs[3] = 512 proofs on 8 GPUs)",
+            "trace_length": n, "blowup": BLOWUP, "proof_options": "42/8/4/None/8/31",
+            "proofs_per_step": per * world,
+            "parallelism": f"dp{world} (independent proofs; RCCL scatter of inputs, gather of proof bytes)",
+            "submission": f"pipelined, depth {args.depth} (xfg_prove_batch_submit / xfg_batch_wait)",
+        },
+        # the exchange step of a sharded run (--dist / N > 1): one scatter of packed inputs per
+        # step and one gather of fixed-size proof records per step, both inside the timed steps
+        "exchange": None if ex is None else {
+            "backend": backend, "scatter": f"one per step, issued {ex.lookahead} steps ahead",
+            "gather": "one per step: fixed record of 8 B lengths + proof-size-bound slots per rank",
+            "record_bytes_per_rank": ex.rec, "proof_size_bound": ex.cap},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
+                     "traffic_source": traffic_src,
+                     # the kernel is VALU-issue-bound: the same launch set
+                     # against the VALU ceiling, instruction counts from the same PMC record
+                     "valu": valu_roofline(pmc, lde_ms, WIDTH * per * n * BLOWUP),
+                     "kernel": "trace LDE (ntt_pass_a_cos2 + ntt_pass_b_tq<8,8,4,split>), 7 columns x "
+                               f"{per} proofs, {lde_ms:.3f} ms/launch-set, {lde_bytes} algorithmic B",
+                     # the same launch sets inside the timed pipelined steps (per XFG_UNIT-proof unit,
+                     # sharing the GPU with the other lanes' kernels)
+                     "in_pipeline": in_pipeline(pipe_ms, pipe_sets, pipe_polys, n)},
+        "whole_proof": whole_proof_line(total / el, n, world),
+        "verified": verified,
+        "verify": vrate,
+        "stage_ms_one_batch": prover_stage,
+        "sync_prove_batch_ms": round(sync_call_ms, 3),
+    }
+    if c5:
+        line["config5"] = c5
+    if world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    print(json.dumps(line), flush=True)
     prover.close()
     if dist is not None:
+        dist.barrier()
         dist.destroy_process_group()
 
 

@@ -1,8 +1,8 @@
 #!/bin/bash
 # GPU box: same-box A/B of the configs[4] side measurement (2^20-step trace LDE at blowup 16 and
 # proofs/s of 4-proof quadratic-extension batches, bench.config5), alternating settings
-# usage: AB="XFG_NTT_XCD=0 XFG_NTT_XCD=1" bash scripts/c5_ab.sh   (XFG_LIB=... works as a setting;
-# a comma joins several variables into one setting: XFG_NTT_LTA=9,XFG_NTT_LTB=9)
+# usage: AB="XFG_LIB=ab/liba.so XFG_LIB=ab/libb.so" bash scripts/c5_ab.sh   (any env setting works;
+# a comma joins several variables into one setting: XFG_LIB=ab/liba.so,XFG_LANES=6)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 for rep in 1 2; do

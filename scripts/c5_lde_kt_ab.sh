@@ -1,10 +1,10 @@
 #!/bin/bash
 # GPU box: per-kernel times (rocprofv3 --kernel-trace --stats) of the configs[4] trace-LDE launch set
-# under NTT knob variants: VARIANTS="name:ENV=..;..."
+# of library builds: VARIANTS="name:XFG_LIB=ab/libX.so;..." (an empty setting = the in-tree build)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
-V="${VARIANTS:-base:;lta8preg:XFG_NTT_LTA=8 XFG_NTT_PREG=1;lta8:XFG_NTT_LTA=8}"
+V="${VARIANTS:-base:}"
 IFS=';' read -ra VS <<< "$V"
 for v in "${VS[@]}"; do
   name="${v%%:*}"; envs="${v#*:}"

@@ -87,6 +87,40 @@ def test_proof_size_bound_covers_oracle_sizes():
         assert lib.xfg_proof_size_bound(C.c_uint64(case["n"]), C.byref(o)) >= case["len"]
 
 
+@pytest.mark.parametrize("n,beta,q,ext,rem", [
+    (8, 2, 15, 1, 1), (64, 4, 200, 1, 7), (64, 4, 255, 2, 7), (256, 8, 42, 1, 31), (256, 16, 128, 2, 3),
+    (1024, 8, 42, 1, 31), (1024, 4, 100, 2, 255), (512, 2, 255, 1, 0)])
+def test_proof_size_bound_is_tight_upper_bound(n, beta, q, ext, rem):
+    """the bound a fixed-size exchange record is sized by (bench.Exchange): never below a real proof
+    (the oracle's, same serialisation), including shapes where the queries fill the Merkle trees"""
+    import xfgstark
+    lib = C.CDLL(xfgstark.LIB_PATH)
+    lib.xfg_proof_size_bound.restype = C.c_size_t
+    o = xfgstark.ProofOptions(q, beta, 0, ext, 8, rem)._c()
+    bound = lib.xfg_proof_size_bound(C.c_uint64(n), C.byref(o))
+    opts = O.options(num_queries=q, blowup=beta, grinding=0, field_extension=ext, fri_rem_max_deg=rem)
+    for i in range(3):
+        kw = synthetic.burn_inputs(i)
+        st, air = O.air_from_inputs(kw["burn_amount"], kw["mint_amount"], kw["tx_prefix_hash"],
+                                    kw["recipient_address"], kw["secret"])
+        st, proof = O.prove(air, n, opts)
+        assert st == 0
+        assert len(proof) <= bound, (len(proof), bound)
+
+
+def test_proof_size_bound_configs2():
+    """configs[2] (2^16, blowup 8, 42/8/4/None/8/31): golden proof ~78 KB, bound within 1.35x"""
+    import json
+    import xfgstark
+    lib = C.CDLL(xfgstark.LIB_PATH)
+    lib.xfg_proof_size_bound.restype = C.c_size_t
+    o = xfgstark.ProofOptions.reference()._c()
+    bound = lib.xfg_proof_size_bound(C.c_uint64(1 << 16), C.byref(o))
+    lens = [c["len"] for c in json.load(open(os.path.join(ROOT, "tests", "golden", "proofs.json")))
+            if c["n"] == 1 << 16 and c["blowup"] == 8 and "options" not in c]
+    assert lens and all(ln <= bound < 1.35 * ln for ln in lens), (lens, bound)
+
+
 def test_no_gpu_means_loud_failure():
     import torch
     import xfgstark

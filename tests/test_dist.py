@@ -1,15 +1,20 @@
-"""Multi-GPU path on CPU: bench.sharded_step over torch.distributed gloo with world_size 2.
+"""Multi-GPU path on CPU: bench.py's exchange step (bench.Exchange + bench.pipelined_steps) over
+torch.distributed gloo with world_size 2 and 4.
 
-Rank 0 scatters packed burn inputs, every rank "proves" its shard (here: the product's host
-marshalling, xfgstark.air_consts, serialised -- variable-length outputs), rank 0 gathers the
-bytes. The result must equal proving the whole batch on one rank, in order (independent proofs
-shard with no data-path collective besides the input scatter / output gather)."""
+Rank 0 holds the packed burn inputs; each step's shard is scattered by its own collective, every
+rank "proves" its shard into a fixed-size exchange record (here: the product's host marshalling,
+xfgstark.air_consts, serialised -- variable-length outputs), rank 0 gathers the records. The result
+must equal proving the whole batch on one rank, in order (independent proofs shard with no
+data-path collective besides the input scatter / output gather)."""
+import ctypes as C
 import os
 import socket
 import struct
 
 import pytest
 import torch.multiprocessing as mp
+
+FAKE_CAP = 400  # record slot of a fake proof (at most 3 x 112 bytes)
 
 
 def _fake_prove(kws):
@@ -22,7 +27,24 @@ def _fake_prove(kws):
     return out
 
 
-def _worker(rank, world, port, per, ret, mode="sync"):
+class _FakeRecordBatch:
+    """a submitted batch writing into an exchange record like PendingBatch.record_ready: int64
+    lengths, then one FAKE_CAP slot per proof; `fail` = index of a proof that fails (length 0)"""
+
+    def __init__(self, kws, record, fail=None):
+        self.kws, (self.addr, self.nbytes), self.fail = kws, record, fail
+
+    def record_ready(self):
+        proofs = _fake_prove(self.kws)
+        k = len(proofs)
+        assert self.nbytes >= 8 * k + k * FAKE_CAP
+        hdr = (C.c_int64 * k).from_address(self.addr)
+        for i, p in enumerate(proofs):
+            hdr[i] = 0 if i == self.fail else len(p)
+            C.memmove(self.addr + 8 * k + i * FAKE_CAP, p, len(p))
+
+
+def _worker(rank, world, port, per, ret, steps=3, depth=2, lookahead=4, fail=None):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     for p in (os.path.join(root, "xfg-stark_amd"), root):
@@ -34,27 +56,27 @@ def _worker(rank, world, port, per, ret, mode="sync"):
     import bench
     import synthetic
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    if mode == "sync":
-        inputs = [synthetic.burn_inputs(i) for i in range(per * world)] if rank == 0 else None
-        out = bench.sharded_step(_fake_prove, inputs, rank, world, per, torch.device("cpu"), dist)
-    else:
-        # bench.py's timed loop: 3 steps, submission depth 2, inputs pre-packed on rank 0
-        batches = [[synthetic.burn_inputs(100 * k + i) for i in range(per * world)] if rank == 0 else None
-                   for k in range(3)]
-        packed = [torch.from_numpy(bench.pack_inputs(b)).view(world, per, bench.REC) if rank == 0 else None
-                  for b in batches]
-        seen = []
+    batches = [[synthetic.burn_inputs(100 * k + i) for i in range(per * world)] if rank == 0 else None
+               for k in range(steps)]
+    packed = [torch.from_numpy(bench.pack_inputs(b)).view(world, per, bench.REC) if rank == 0 else None
+              for b in batches]
+    seen = []
 
-        def submit(kws):
-            seen.append(len(kws))
-            return _fake_prove(kws)
+    def submit(kws, record):
+        seen.append(len(kws))
+        return _FakeRecordBatch(kws, record, fail if rank == world - 1 else None)
 
-        depth = 3 if mode == "pipelined3" else 2
-        out = bench.pipelined_steps(submit, lambda p: p, batches, rank, world, per, torch.device("cpu"), dist,
-                                    packed, depth)
-        assert seen == [per] * 3
+    ex = bench.Exchange(rank, world, per, FAKE_CAP, torch.device("cpu"), dist, send_slots=depth + 3,
+                        lookahead=lookahead)
+    try:
+        out = bench.pipelined_steps(submit, None, batches, depth, ex, packed)
+    except RuntimeError as e:
+        ret.put(("error", str(e)))
+        out = "raised"
+    assert seen == [per] * steps
     if rank == 0:
-        ret.put([bytes(x) for x in out])  # rank 0 holds zero-copy views into the gathered buffer
+        if out != "raised":
+            ret.put(("ok", [bytes(x) for x in out]))  # rank 0 holds zero-copy views into the ring
     else:
         assert out is None
     dist.barrier()
@@ -69,22 +91,40 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("world,per,mode", [(2, 3, "sync"), (2, 1, "sync"), (2, 2, "pipelined"), (2, 2, "pipelined3")])
-def test_sharded_step_gloo(world, per, mode):
-    import synthetic
+def _run(world, per, **kw):
     ctx = mp.get_context("spawn")
     ret = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, per, ret, mode)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, per, ret), kwargs=kw) for r in range(world)]
     for p in procs:
         p.start()
     out = ret.get(timeout=120)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    base = 200 if mode.startswith("pipelined") else 0  # pipelined: the last of 3 steps
+    return out
+
+
+@pytest.mark.parametrize("world,per,steps,depth,lookahead", [
+    (2, 3, 1, 1, 4),   # one synchronous step
+    (2, 1, 3, 2, 1),   # scatter only one step ahead
+    (2, 2, 3, 2, 4),   # lookahead past the window
+    (2, 2, 5, 3, 2),
+    (4, 2, 4, 2, 3),   # four ranks
+])
+def test_exchange_gloo(world, per, steps, depth, lookahead):
+    import synthetic
+    kind, out = _run(world, per, steps=steps, depth=depth, lookahead=lookahead)
+    assert kind == "ok"
+    base = 100 * (steps - 1)  # the last step's inputs, in rank order
     want = _fake_prove([synthetic.burn_inputs(base + i) for i in range(per * world)])
     assert out == want
+
+
+def test_exchange_failed_proof_raises_on_rank0():
+    """a proof that failed on another rank (length 0 in its record) must not be read as a proof"""
+    kind, msg = _run(2, 2, steps=2, depth=2, fail=1)
+    assert kind == "error" and "rank 1 proof 1" in msg
 
 
 def test_pack_unpack_roundtrip():
@@ -94,26 +134,27 @@ def test_pack_unpack_roundtrip():
     assert bench.unpack_inputs(bench.pack_inputs(kws)) == kws
 
 
+class _Work:
+    def wait(self):
+        pass
+
+
 class _LoopbackDist:
-    """two "ranks" in one process: rank 1's payload is handed to rank 0's gather (exercises the
-    device-tensor branch of bench.gather_proofs on one GPU)"""
-    class ReduceOp:
-        MAX = "max"
+    """two "ranks" in one process, seen from rank 0: rank 1's record is handed to rank 0's gather
+    and rank 0's scatter keeps chunk 0 (exercises the device-tensor branch of bench.Exchange --
+    side stream, pinned records, events -- on one GPU)"""
 
     def __init__(self, other):
         self.other = other
 
-    def all_reduce(self, t, op=None):
-        t.copy_(torch_max(t, self.other["size"]))
+    def scatter(self, t, chunks, src=0, async_op=False):
+        t.copy_(chunks[0])
+        return _Work()
 
-    def gather(self, t, got, dst=0):
+    def gather(self, t, got, dst=0, async_op=False):
         got[0].copy_(t)
-        got[1].copy_(self.other["payload"].to(t.device))
-
-
-def torch_max(a, b):
-    import torch
-    return torch.maximum(a, b.to(a.device))
+        got[1].copy_(self.other.to(t.device))
+        return _Work()
 
 
 def _read_dump(path):
@@ -166,31 +207,43 @@ def test_bench_two_ranks_real_prover(tmp_path):
 
 
 @pytest.mark.gpu
-def test_gather_proofs_device_branch():
+def test_exchange_device_branch():
     import sys
     import numpy as np
     import torch
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, root)
     import bench
-    per = 3
-    mine = [bytes([i]) * (100 + 37 * i) for i in range(per)]
+    import synthetic
+    per, cap, dev = 3, 400, torch.device("cuda", 0)
+    kws = [synthetic.burn_inputs(i) for i in range(2 * per)]
     theirs = [bytes([50 + i]) * (300 - 11 * i) for i in range(per)]
-    # rank 1's payload as gather_proofs builds it, padded to the common size
-    hdr = 8 * per
-    size = max(hdr + sum(map(len, mine)), hdr + sum(map(len, theirs)))
-    pay = np.zeros(size, dtype=np.uint8)
-    pay[:hdr] = np.array([len(p) for p in theirs], dtype=np.int64).view(np.uint8)
-    pay[hdr:hdr + sum(map(len, theirs))] = np.frombuffer(b"".join(theirs), dtype=np.uint8)
-    other = {"size": torch.tensor([size], dtype=torch.int64), "payload": torch.from_numpy(pay)}
-    out = bench.gather_proofs(mine, 0, 2, per, torch.device("cuda", 0), _LoopbackDist(other))
-    assert [bytes(x) for x in out] == mine + theirs
+    pay = np.zeros(8 * per + per * cap, dtype=np.uint8)  # rank 1's record: lengths, fixed slots
+    pay[:8 * per] = np.array([len(p) for p in theirs], dtype=np.int64).view(np.uint8)
+    for i, p in enumerate(theirs):
+        pay[8 * per + i * cap:8 * per + i * cap + len(p)] = np.frombuffer(p, dtype=np.uint8)
+    ex = bench.Exchange(0, 2, per, cap, dev, _LoopbackDist(torch.from_numpy(pay)), send_slots=3, lookahead=2)
+    packed = [torch.from_numpy(bench.pack_inputs(kws)).to(dev).view(2, per, bench.REC)] * 3
+    ex.start_inputs(packed, 3)
+    for step in range(3):
+        assert ex.inputs(step) == kws[:per]  # rank 0's shard of each step
+        s, addr, nbytes = ex.claim()
+        assert nbytes == len(pay)
+        k = len(kws[:per])
+        mine = _fake_prove(kws[:per])
+        hdr = (C.c_int64 * k).from_address(addr)
+        for i, p in enumerate(mine):
+            hdr[i] = len(p)
+            C.memmove(addr + 8 * k + i * cap, p, len(p))
+        out = ex.gather(s).proofs()
+        assert [bytes(x) for x in out] == mine + theirs
+    ex.drain()
 
 
 @pytest.mark.gpu
 def test_bench_rccl_collectives_one_rank():
-    """bench.py's exchange step over RCCL itself (backend nccl: device tensors, scatter of packed
-    inputs, length all-reduce, padded gather, pinned D2H of the gathered proofs), one rank on the
+    """bench.py's exchange step over RCCL itself (backend nccl: device tensors, one scatter of packed
+    inputs per step, gather of fixed-size proof records, pinned D2H), one rank on the
     one-GPU box through torch.distributed.run -- the path the driver's multi-GPU runs take. bench.py
     --dist checks that the gathered proofs equal a direct prove_batch of the same inputs."""
     import json
@@ -205,3 +258,53 @@ def test_bench_rccl_collectives_one_rank():
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 1 and line["steps"] == 2 and line["value"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_config3_eight_ranks_real_prover(tmp_path):
+    """BASELINE configs[3] at its workload: 512 burn proofs per step (2^16-step traces, blowup 8, the
+    reference options) sharded over EIGHT bench.py ranks under torch.distributed.run, 64 proofs per
+    rank, all sharing the one GPU (XFG_DIST_BACKEND=gloo: RCCL cannot put two ranks on one device;
+    the driver's 8-GPU node runs the same code over nccl). Rank 0 GPU-verifies all 512 gathered
+    proofs of the last step against the statements of the inputs in rank order and (--dist) compares
+    them byte for byte with a direct prove_batch of the same 512 inputs; here the first proof of
+    every rank's shard must equal the oracle's bytes and all 512 must pass the oracle verifier.
+    Reference batch pattern: src/burn_mint_verifier.rs:326-338, harness src/benchmarks/mod.rs:301-342."""
+    import json
+    import subprocess
+    import sys
+    from concurrent.futures import ThreadPoolExecutor
+    import oracle_lib as O
+    import synthetic
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    dump = tmp_path / "proofs.bin"
+    per, world, steps, warmup, n = 64, 8, 2, 1, 1 << 16
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", str(world), "--steps", str(steps), "--warmup", str(warmup), "--per-gpu", str(per),
+           "--log-n", "16", "--depth", "2", "--no-cpu-baseline", "--no-config5", "--dist",
+           "--dump-proofs", str(dump)]
+    # 3 lanes per rank: 8 contexts share the card's memory and hardware queues
+    env = dict(os.environ, XFG_DIST_BACKEND="gloo", XFG_LANES="3", OMP_NUM_THREADS="2")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=840, cwd=root, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == world and line["config"]["proofs_per_step"] == 512
+    assert line["verified"] == per * world
+    got = _read_dump(dump)
+    assert len(got) == per * world
+    last = [synthetic.burn_inputs((warmup + steps - 1) * per * world + i) for i in range(per * world)]
+    airs = []
+    for kw in last:
+        st, air = O.air_from_inputs(kw["burn_amount"], kw["mint_amount"], kw["tx_prefix_hash"],
+                                    kw["recipient_address"], kw["secret"])
+        assert st == 0
+        airs.append(air)
+    opts = O.options()
+    with ThreadPoolExecutor(16) as pool:
+        verdicts = list(pool.map(lambda i: O.verify(airs[i], got[i], opts), range(len(got))))
+        firsts = list(pool.map(lambda q: O.prove(airs[q * per], n, opts), range(world)))
+    assert verdicts == [0] * len(got)
+    for q, (st, want) in enumerate(firsts):  # the first proof of each rank's shard
+        assert st == 0 and got[q * per] == want, q

@@ -494,3 +494,79 @@ def test_submit_rejects_empty_and_unsized_batches(prover):
         prover.submit_batch([], trace_length=1024).result()
     with pytest.raises(xfgstark.XfgStarkError):
         prover.submit_batch([synthetic.burn_inputs(1)], trace_length=100).result()
+
+
+_KNOB_CHILD = r"""
+import hashlib, sys
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+import synthetic, xfgstark
+pr = xfgstark.XfgBurnMintProver()
+for n in (1024, 1 << 16):
+    res = pr.prove_batch([synthetic.burn_inputs(700 + i) for i in range(12)], trace_length=n)
+    print(n, " ".join(hashlib.sha256(r.to_bytes()).hexdigest() for r in res))
+"""
+
+
+def test_env_knobs_keep_proof_bytes(prover, tmp_path):
+    """every environment knob the library still reads (XFG_LANES, XFG_UNIT, XFG_SPLIT_MIN,
+    XFG_HOST_THREADS, XFG_TRACE) changes scheduling only: a child process with non-default values
+    (2 lanes, 5-proof units split down to 2, 1 host thread, host traces on) emits the same 12 proofs
+    at n = 2^10 and 2^16 as this process at the defaults, and the first proof equals the oracle's"""
+    import subprocess
+    import sys
+    import xfgstark
+    prover._options = xfgstark.ProofOptions.reference()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, XFG_LANES="2", XFG_UNIT="5", XFG_SPLIT_MIN="2", XFG_HOST_THREADS="1", XFG_TRACE="1")
+    r = subprocess.run([sys.executable, "-c", _KNOB_CHILD, os.path.join(root, "xfg-stark_amd"), root],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stderr.strip(), "XFG_TRACE=1 printed no host trace"
+    got = {int(line.split()[0]): line.split()[1:] for line in r.stdout.strip().splitlines()}
+    for n in (1024, 1 << 16):
+        kws = [synthetic.burn_inputs(700 + i) for i in range(12)]
+        want = [p.to_bytes() for p in prover.prove_batch(kws, trace_length=n)]
+        assert got[n] == [hashlib.sha256(b).hexdigest() for b in want], n
+    st, oracle = O.prove(oracle_air(synthetic.burn_inputs(700)), 1024, O.options())
+    assert st == 0 and hashlib.sha256(oracle).hexdigest() == got[1024][0]
+
+
+def test_batch_record_and_consumption_rules(prover):
+    """submit_batch_record writes proofs and lengths straight into a caller's fixed-size record (the
+    exchange format of bench.Exchange); a batch is consumed once: result() after packed_into() or
+    record_ready() raises instead of returning an empty list"""
+    import ctypes as C
+    import xfgstark
+    prover._options = xfgstark.ProofOptions.reference()
+    n, k = 1024, 5
+    kws = [synthetic.burn_inputs(900 + i) for i in range(k)]
+    want = [p.to_bytes() for p in prover.prove_batch(kws, trace_length=n)]
+    size = xfgstark.record_size(k, n, prover._options)
+    cap = prover.proof_size_bound(n)
+    assert size == 8 * k + k * cap
+    rec = (C.c_uint8 * size)()
+    p = prover.submit_batch_record(kws, n, C.addressof(rec), size)
+    assert p.record_ready() == size
+    raw = bytes(rec)
+    lens = np.frombuffer(raw[:8 * k], dtype=np.int64)
+    assert [raw[8 * k + i * cap:8 * k + i * cap + int(lens[i])] for i in range(k)] == want
+    with pytest.raises(xfgstark.XfgStarkError):
+        p.result()
+    with pytest.raises(xfgstark.XfgStarkError):  # too small a record
+        prover.submit_batch_record(kws, n, C.addressof(rec), size - 1)
+    q = prover.submit_batch(kws, trace_length=n)
+    dst = np.zeros(8 * k + sum(map(len, want)), dtype=np.uint8)
+    assert q.packed_into(dst) == dst.size
+    with pytest.raises(xfgstark.XfgStarkError):
+        q.result()
+    with pytest.raises(xfgstark.XfgStarkError):
+        q.record_ready()
+    r = prover.submit_batch(kws, trace_length=n)
+    assert [x.to_bytes() for x in r.result()] == want and r.result() is r.result()
+    with pytest.raises(xfgstark.XfgStarkError):
+        r.packed_into(dst)
+    s = prover.submit_batch(kws, trace_length=n)
+    free = len(prover._free)
+    assert s.wait() == 0
+    del s  # waited but never consumed: its buffer returns to the pool
+    assert len(prover._free) == free + 1

@@ -271,15 +271,9 @@ __global__ __launch_bounds__(64) void open_rows_kernel(const u64* lde, const u64
         default: break;                                                                         \
     }
 
-// in-block Merkle levels continue while a level keeps >= XFG_UP_WMIN nodes per block (default 64:
-// full waves only); the narrower levels go to launch_tree_top
-static int up_wmin(u64 T) {
-    static const int v = [] {
-        const char* e = getenv("XFG_UP_WMIN");
-        return e && *e ? std::max(1, atoi(e)) : 64;
-    }();
-    return (int)std::min<u64>(T, (u64)v);
-}
+// in-block Merkle levels continue while a level keeps >= 64 nodes per block (full waves only); the
+// narrower levels go to launch_tree_top
+static int up_wmin(u64 T) { return (int)std::min<u64>(T, 64); }
 u64 launch_leaves_lde(const u64* lde, int nc, Digest* nodes, u64 node_stride, int npoly, int logn, int logbeta,
                       hipStream_t s) {
     const u64 n = 1ULL << logn, T = std::min<u64>(256, n / 2);

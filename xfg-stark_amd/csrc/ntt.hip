@@ -250,8 +250,6 @@ struct NttArgs {
     int xcd;        // 1: XCD-contiguous block order (see xcd_block)
     int tq_b;       // forward: pass B applies the four-step twiddles as it loads (ntt_pass_a_cos)
     int preg;       // forward pass A: coset pre-factors read from the pass tables in L2, not LDS
-    int yblk;       // forward, no four-step table: the intermediate is stored in column blocks of
-                    // 2^yblk columns ([j2 >> yblk][k1][j2 & mask]) instead of rows [k1][j2]
     Tables T;
 };
 
@@ -358,14 +356,9 @@ __global__ __launch_bounds__(1 << LOGT, (1 << (10 - LOGT)) >> (LOGE - 4)) void n
         }
         u64 w = INV ? wq[q] : gl_mul(p7q[q], wq[q]);
         const u64 step = sq[q];
-        // blocked intermediate: this column's block, rows of 2^yblk words (whole lines per store
-        // instruction however narrow the tile)
-        const int B = a.yblk;
-        const u64 cb = B ? ((j2 >> B) << (a.logR + B)) + (j2 & ((1u << B) - 1)) : j2;
-        const int rs = B ? B : a.logC;
 #pragma unroll
         for (int r = 0; r < RR; r++) {
-            y[((u64)(base + r * stride) << rs) + cb] = gl_mul(v[r], w);
+            y[((u64)(base + r * stride) << a.logC) + j2] = gl_mul(v[r], w);
             if (r + 1 < RR) w = gl_mul(w, step);
         }
     };
@@ -547,11 +540,6 @@ __global__ __launch_bounds__(1 << LOGT) void ntt_pass_b(NttArgs a) {
             if (tqb) return gl_mul(yv[o / G1], tv[o / G1]);
         }
         const u64 i = ((u64)(k10 + seq) << LOGC) + j + o;
-        if (!INV && a.yblk) {  // blocked intermediate (pass A stored column blocks)
-            const int B = a.yblk;
-            const u64 j2 = (u64)(j + o);
-            return y[((j2 >> B) << (a.logR + B)) + ((u64)(k10 + seq) << B) + (j2 & ((1u << B) - 1))];
-        }
         return tqb ? gl_mul(y[i], tqb[i]) : y[i];
     };
     const auto rout = buf_rsrc(a.out + (u64)pt * n + k10);
@@ -580,8 +568,9 @@ __global__ __launch_bounds__(1 << LOGT) void ntt_pass_b(NttArgs a) {
 // ---------------------------------------------------------------- pass B, forward with the four-step table
 // ntt_pass_b specialised to the path every tabled LDE takes (the all-coset pass A left the four-step
 // twiddles to it): one first-step group per thread, data and table loaded up front, no run-time
-// branches for the other paths
-template <int LOGC, int LOGT, int LOGE, bool SPLIT = false>
+// branches for the other paths; the exchange between its two steps goes through the LDS tile in
+// 32-bit halves (pass_dft_split)
+template <int LOGC, int LOGT, int LOGE>
 __global__ __launch_bounds__(1 << LOGT) void ntt_pass_b_tq(NttArgs a) {
     constexpr int C = 1 << LOGC, RR = Plan<LOGC, LOGE>::LAST_R, NT = 1 << LOGT;
     using PLB = Plan<LOGC, LOGE>;
@@ -592,7 +581,7 @@ __global__ __launch_bounds__(1 << LOGT) void ntt_pass_b_tq(NttArgs a) {
     const int TR = 1 << logTR;
     u64* tile = lds;
     const int tw = TR * row_pitch(C, LOGE, LOGT + LOGE - LOGC);
-    u64* ltw = SPLIT ? reinterpret_cast<u64*>(reinterpret_cast<u32*>(lds) + tw) : lds + tw;
+    u64* ltw = reinterpret_cast<u64*>(reinterpret_cast<u32*>(lds) + tw);
     int bx, by;
     xcd_block(a.xcd & 2, bx, by);
     const int pt = by, k10 = bx * TR;
@@ -619,10 +608,7 @@ __global__ __launch_bounds__(1 << LOGT) void ntt_pass_b_tq(NttArgs a) {
         for (int r = 0; r < RR; r++)
             buf_st(rout, (seq + ((u32)base << a.logR)) * 8, ((u32)(r * stride) << a.logR) * 8, canon(v[r]));
     };
-    if constexpr (SPLIT)
-        pass_dft_split<LOGC, LOGE, false, false, NT>(reinterpret_cast<u32*>(tile), logTR, ltw, ldg, stg, NoPf{});
-    else
-        pass_dft<LOGC, LOGE, false, false, NT>(tile, logTR, ltw, ldg, stg, NoPf{});
+    pass_dft_split<LOGC, LOGE, false, false, NT>(reinterpret_cast<u32*>(tile), logTR, ltw, ldg, stg, NoPf{});
 }
 
 // ---------------------------------------------------------------- pass B, persistent (forward, no table)
@@ -634,10 +620,8 @@ __global__ __launch_bounds__(1 << LOGT) void ntt_pass_b_tq(NttArgs a) {
 // Tiles are dealt per XCD in contiguous ranges (the blocks of XCD x = blockIdx % 8 walk the x-th
 // eighth of the tiles side by side), so the 64-byte output runs of neighbouring tiles meet in
 // one L2, as xcd_block arranges for the one-tile form.
-template <int LOGC, int LOGT, int LOGE, int TQ, int MINW>
+template <int LOGC, int LOGT, int LOGE, int MINW>
 __global__ __launch_bounds__(1 << LOGT, MINW) void ntt_pass_b_pers(NttArgs a, int ntx, int ntiles) {
-    // TQ: 0 no four-step table (configs[4]); 1 table twiddles loaded per tile; 2 table twiddles
-    // prefetched with the data (the four-step table has the intermediate's [k1][j2] layout)
     constexpr int C = 1 << LOGC, RR = Plan<LOGC, LOGE>::LAST_R, NT = 1 << LOGT;
     using PLB = Plan<LOGC, LOGE>;
     constexpr int R1 = 1 << PLB::FIRST_LOGR, G1 = C / R1;
@@ -655,39 +639,20 @@ __global__ __launch_bounds__(1 << LOGT, MINW) void ntt_pass_b_pers(NttArgs a, in
     const int per_x = gridDim.x >> 3, x = blockIdx.x & 7, slot = blockIdx.x >> 3;
     const int span = (ntiles + 7) >> 3, tend = min((x + 1) * span, ntiles);
     const int seq0 = threadIdx.x / G1, j0 = threadIdx.x % G1;
-    const int bmask = (1 << a.logbeta) - 1;
-    auto load = [&](int ti, u64* dst, u64* tdst) {
+    auto load = [&](int ti, u64* dst) {
         const int pt = ti / ntx, k10 = (ti - pt * ntx) * TR;
-        const u64 i0 = ((u64)(k10 + seq0) << LOGC) + j0;
-        const u64* y = a.y + (u64)pt * n + i0;
+        const u64* y = a.y + (u64)pt * n + ((u64)(k10 + seq0) << LOGC) + j0;
 #pragma unroll
         for (int r = 0; r < R1; r++) dst[r] = y[r * G1];
-        if constexpr (TQ != 0) {
-            const u64* tq = a.t4 + ((u64)(pt & bmask) << a.logn) + i0;
-#pragma unroll
-            for (int r = 0; r < R1; r++) tdst[r] = tq[r * G1];
-        }
     };
     int ti = x * span + slot;
-    u64 yv[R1], tv[TQ ? R1 : 1];
-    if (ti < tend) load(ti, yv, tv);
+    u64 yv[R1];
+    if (ti < tend) load(ti, yv);
     for (; ti < tend; ti += per_x) {
         const int pt = ti / ntx, k10 = (ti - pt * ntx) * TR;
-        u64 nx[R1], ntq[TQ == 2 ? R1 : 1];
-        if (ti + per_x < tend) {
-            if constexpr (TQ == 2) load(ti + per_x, nx, ntq);
-            else {
-                const u64* y = a.y + (u64)((ti + per_x) / ntx) * n;
-                const int k1n = ((ti + per_x) % ntx) * TR;
-                const u64 i0 = ((u64)(k1n + seq0) << LOGC) + j0;
-#pragma unroll
-                for (int r = 0; r < R1; r++) nx[r] = y[i0 + r * G1];
-            }
-        }
-        auto ldg = [&](int, int, int o) -> u64 {
-            if constexpr (TQ != 0) return gl_mul(yv[o / G1], tv[o / G1]);
-            return yv[o / G1];
-        };
+        u64 nx[R1];
+        if (ti + per_x < tend) load(ti + per_x, nx);
+        auto ldg = [&](int, int, int o) -> u64 { return yv[o / G1]; };
         const auto rout = buf_rsrc(a.out + (u64)pt * n + k10);
         auto stg = [&](int, int seq, int base, int stride, u64* v) {
 #pragma unroll
@@ -697,17 +662,6 @@ __global__ __launch_bounds__(1 << LOGT, MINW) void ntt_pass_b_pers(NttArgs a, in
         pass_dft<LOGC, LOGE, false, false, NT>(tile, logTR, ltw, ldg, stg, [](int, int, int, int) {});
 #pragma unroll
         for (int r = 0; r < R1; r++) yv[r] = nx[r];
-        if constexpr (TQ == 2) {
-#pragma unroll
-            for (int r = 0; r < R1; r++) tv[r] = ntq[r];
-        } else if constexpr (TQ == 1) {
-            if (ti + per_x < tend) {
-                const int pn = (ti + per_x) / ntx, k1n = ((ti + per_x) % ntx) * TR;
-                const u64* tq = a.t4 + ((u64)(pn & bmask) << a.logn) + ((u64)(k1n + seq0) << LOGC) + j0;
-#pragma unroll
-                for (int r = 0; r < R1; r++) tv[r] = tq[r * G1];
-            }
-        }
     }
 }
 
@@ -822,15 +776,9 @@ static void run_pass_b(int logC, int logT, int logE, dim3 g, size_t lds, hipStre
 #undef XFG_NTT_LAUNCH
 
 // split n = R * C: evenly below 2^18, C = 2R from 2^18 on except 2^20 (faster at 2^18; see
-// scripts/ntt_split.py); XFG_NTT_LOGC forces log2(C) for tuning sweeps
+// scripts/ntt_split.py; at 2^24 the splits C = 512 / 2048 / 4096 measured slower than 1024)
 static void ntt_split(int logn, int& logR, int& logC) {
-    static const int force_logc = [] {
-        const char* v = getenv("XFG_NTT_LOGC");
-        return v && *v ? atoi(v) : 0;
-    }();
-    if (force_logc > 1 && force_logc <= 12 && logn - force_logc >= 1 && logn - force_logc <= 10) {
-        logC = force_logc;
-    } else if (logn >= 18) {
+    if (logn >= 18) {
         logC = logn == 20 ? 10 : logn / 2 + 1;  // 2^20: R = C = 1024, both passes wide-tiled (3 % faster)
     } else {
         logC = logn - logn / 2;
@@ -913,192 +861,88 @@ void build_fourstep(u64* out, int logn, int logbeta, const Tables& T, hipStream_
                        logbeta, logR, logC, T);
 }
 
-static int env_knob(const char* name, int dflt) {
-    const char* v = getenv(name);
-    return v && *v ? atoi(v) : dflt;
-}
 static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
     ntt_split(a.logn, a.logR, a.logC);
     const int R = 1 << a.logR, C = 1 << a.logC;
-    // wide tiles (1024 threads, 16384 elements) where a 4096-element tile would hold fewer than 16
-    // columns (pass A, R >= 512) or rows (pass B, C >= 512): the scattered stores then write whole
-    // 128 B lines (XFG_NTT_WIDE=0 disables, for A/B runs)
-    static const bool wide_on = [] {
-        const char* v = getenv("XFG_NTT_WIDE");
-        return !(v && *v == '0');
-    }();
-    // XFG_NTT_LTA / XFG_NTT_LTB force log2(threads) 8, 9 or 10 of the wide-capable passes (sweeps)
-    static const int force_lta = [] {
-        const char* v = getenv("XFG_NTT_LTA");
-        return v && *v ? atoi(v) : 0;
-    }();
-    static const int force_ltb = [] {
-        const char* v = getenv("XFG_NTT_LTB");
-        return v && *v ? atoi(v) : 0;
-    }();
-    // radix-32 steps (32 elements per thread) for pass sizes 2^9 and 2^10: 16 x 32 and 32 x 32
-    // instead of 2 x 16 x 16 and 4 x 16 x 16, one general-twiddle step fewer (XFG_NTT_E=4 disables)
-    static const bool e5_on = [] {
-        const char* v = getenv("XFG_NTT_E");
-        return !(v && *v == '4');
-    }();
-    // XFG_NTT_EA=4 / XFG_NTT_EB=4: radix-16 in pass A / pass B only (A/B knobs)
-    static const bool e5a = [] {
-        const char* v = getenv("XFG_NTT_EA");
-        return !(v && *v == '4');
-    }();
-    static const bool e5b = [] {
-        const char* v = getenv("XFG_NTT_EB");
-        return !(v && *v == '4');
-    }();
-    const int eA = (e5_on && e5a && wide_on && a.logR >= 9 && a.logR <= 10 && a.logC >= 4) ? 5 : 4;
-    const int eB = (e5_on && e5b && wide_on && a.logC >= 9 && a.logC <= 10 && a.logR >= 3) ? 5 : 4;
+    // Pass shapes (the alternatives named there measured slower on the box):
+    // * radix-32 steps (32 elements per thread) for pass sizes 2^9 and 2^10: 16 x 32 and 32 x 32
+    //   instead of 2 x 16 x 16 and 4 x 16 x 16, one general-twiddle step fewer;
+    // * wide tiles (1024 threads, 16384 elements) where a 4096-element radix-16 tile would hold fewer
+    //   than 16 columns (pass A, R >= 512) or rows (pass B, C >= 512), so the scattered stores write
+    //   whole 128 B lines; pass B at C <= 1024 runs 512-thread blocks (8192 elements, <= 78 KiB, two
+    //   blocks per CU: one block's barriers and loads hide behind the other's butterflies);
+    // * radix-32 tiles: pass A 16 columns (512 threads at R = 1024, 256 at R = 512; the forward
+    //   R = 1024 pass of configs[4] 256 threads x 8 columns with the coset pre-factors read from L2 --
+    //   76 KiB of LDS, two blocks per CU), pass B 8192 elements (256 threads, two blocks per CU).
+    const int eA = (a.logR >= 9 && a.logR <= 10 && a.logC >= 4) ? 5 : 4;
+    const int eB = (a.logC >= 9 && a.logC <= 10 && a.logR >= 3) ? 5 : 4;
     const bool capA = a.logR >= 9 && a.logR <= 10 && a.logC >= 4, capB = a.logC >= 9 && a.logC <= 11 && a.logR >= 4;
-    int ltA = capA ? (force_lta >= 8 && force_lta <= 10 ? force_lta : (wide_on ? 10 : 8)) : 8;
-    // pass B: 512 threads (8192 elements, <= 78 KiB, two blocks per CU) up to C = 1024 -- the second
-    // block hides the first one's barriers and load latency; 1024 threads at C = 2048
-    int ltB = capB ? (force_ltb >= 8 && force_ltb <= 10 ? force_ltb : (wide_on ? (a.logC <= 10 ? 9 : 10) : 8)) : 8;
-    // radix-32 tiles: pass A 16 columns (512 threads at R = 1024, 256 at R = 512), pass B 8192
-    // elements (256 threads, two blocks per CU); forced thread counts limited to 256 / 512
-    // (forward R = 1024, configs[4]: 256 threads x 8 columns with the coset pre-factors read from L2
-    // -- 76 KiB of LDS, two blocks per CU -- pass A 828 -> 790 us per 2^24-point trace LDE, same box)
-    if (eA == 5) ltA = (force_lta == 8 || force_lta == 9) ? force_lta : (!inv && a.logR == 10 && a.pt ? 8 : a.logR - 1);
-    if (eB == 5) ltB = (force_ltb == 8 || force_ltb == 9) ? force_ltb : 8;
+    int ltA = capA ? 10 : 8;
+    int ltB = capB ? (a.logC <= 10 ? 9 : 10) : 8;
+    if (eA == 5) ltA = (!inv && a.logR == 10 && a.pt) ? 8 : a.logR - 1;
+    if (eB == 5) ltB = 8;
     const int logTC = a.logC < ltA + eA - a.logR ? a.logC : ltA + eA - a.logR;
     const int logTR = a.logR < ltB + eB - a.logC ? a.logR : ltB + eB - a.logC;
     const int ncos = inv ? 1 : (1 << a.logbeta);
-    // forward pass A of radix-32 tiles reads its coset pre-factors from the pass tables (L2) instead
-    // of an LDS copy: R words less LDS per block (XFG_NTT_PREG=0 / 1 forces it off / on elsewhere)
-    static const int preg_env = [] {
-        const char* v = getenv("XFG_NTT_PREG");
-        return v && *v ? atoi(v) : -1;
-    }();
-    const bool preg_dflt = eA == 5 && ltA == 8 && a.logR == 10;
-    a.preg = (!inv && a.pt && !(a.t4 && a.logR == 8 && ltA == 8 && eA == 4) &&  // (not the cos kernel)
-              (preg_env < 0 ? preg_dflt : preg_env == 1)) ? 1 : 0;
+    a.preg = (!inv && a.pt && eA == 5 && ltA == 8 && a.logR == 10) ? 1 : 0;
     size_t lds_a = ((size_t)(1 << logTC) * row_pitch(R, eA, ltA + eA - a.logR) + (a.preg ? 1 : 2) * R) * sizeof(u64);
     size_t lds_b = ((size_t)(1 << logTR) * row_pitch(C, eB, ltB + eB - a.logC) + C) * sizeof(u64);
     dim3 ga(C >> logTC, npoly * ncos), gb(R >> logTR, npoly * ncos);
-    // tile rows narrower than 16 words (a 128 B line) in the scattered writes: pass A stores TC
-    // consecutive words per row, pass B TR (XFG_NTT_XCD=0 disables, for A/B runs)
-    static const bool xcd_on = [] {
-        const char* v = getenv("XFG_NTT_XCD");
-        return !(v && *v == '0');
-    }();
-    // XFG_NTT_YBLK=1: forward LDE without a four-step table stores the intermediate in column blocks
-    // of the pass-A tile width (A/B knob)
-    static const bool yblk_on = [] {
-        const char* v = getenv("XFG_NTT_YBLK");
-        return v && *v == '1';
-    }();
-    a.yblk = (!inv && !a.t4 && yblk_on) ? logTC : 0;
-    a.xcd = xcd_on ? ((logTC < 4 && !a.yblk ? 1 : 0) | (logTR < 4 ? 2 : 0)) : 0;
+    // XCD-contiguous block order where a tile row of the scattered writes is narrower than a 128 B
+    // line: pass A stores TC consecutive words per row, pass B TR (xcd_block)
+    a.xcd = (logTC < 4 ? 1 : 0) | (logTR < 4 ? 2 : 0);
     if (inv) {
         run_pass_a<true>(a.logR, ltA, eA, ga, lds_a, s, a);
         run_pass_b<true>(a.logC, ltB, eB, gb, lds_b, s, a);
-    } else {
-        // pass B of the tabled LDE with the 32-bit split exchange (pass_dft_split): 19.5 instead of 37 KiB
-        // of LDS per block, 6 instead of 4 waves per SIMD at 77 VGPRs. Same box, pass B 919-942 vs
-        // 946-961 us per 64-proof launch set, bench 12,760 vs 12,699 (5 interleaved runs).
-        // XFG_NTT_SPLIT=0 disables (A/B knob). (Pass A split: 4 waves still, VGPR-bound; neutral.)
-        static const bool split_b = env_knob("XFG_NTT_SPLIT", 1) != 0;
-        // all cosets of a column tile in one block (ntt_pass_a_cos); XFG_NTT_COS=0 disables
-        static const bool cos_on = [] {
-            const char* v = getenv("XFG_NTT_COS");
-            return !(v && *v == '0');
-        }();
-        // shift-twisted cosets (ntt_pass_a_cos2) where its tables exist; XFG_NTT_COS2=0 disables
-        static const bool cos2_on = [] {
-            const char* v = getenv("XFG_NTT_COS2");
-            return !(v && *v == '0');
-        }();
-        if (cos_on && cos2_on && a.t4 && a.logR == 8 && ltA == 8 && eA == 4 && !(a.xcd & 1) && a.logbeta >= 2) {
-            a.tq_b = 1;
-            static const size_t pad_a = (size_t)std::max(0, env_knob("XFG_NTT_APAD", 0));  // occupancy probe
-            hipLaunchKernelGGL(ntt_pass_a_cos2, dim3(C >> logTC, npoly), dim3(256), lds_a + pad_a, s, a);
-        } else if (cos_on && a.t4 && a.logR == 8 && ltA == 8 && eA == 4 && !(a.xcd & 1)) {
-            a.tq_b = 1;
+        return;
+    }
+    // pass A: all cosets of a column tile in one block where the four-step table exists (R = 256):
+    // shift-twisted cosets (ntt_pass_a_cos2) for beta >= 4, per-coset pre-factors (ntt_pass_a_cos) at
+    // beta = 2; the four-step twiddles are then applied by pass B as it loads (tq_b)
+    if (a.t4 && a.logR == 8 && ltA == 8 && eA == 4 && !(a.xcd & 1)) {
+        a.tq_b = 1;
+        if (a.logbeta >= 2)
+            hipLaunchKernelGGL(ntt_pass_a_cos2, dim3(C >> logTC, npoly), dim3(256), lds_a, s, a);
+        else
             hipLaunchKernelGGL(ntt_pass_a_cos<8>, dim3(C >> logTC, npoly), dim3(256), lds_a, s, a);
-        } else
-            run_pass_a<false>(a.logR, ltA, eA, ga, lds_a, s, a);
-        // persistent pass B past the four-step tables (XFG_NTT_BPERS=0 disables, for A/B runs)
-        static const bool bpers_on = [] {
-            const char* v = getenv("XFG_NTT_BPERS");
-            return !(v && *v == '0');
+    } else {
+        run_pass_a<false>(a.logR, ltA, eA, ga, lds_a, s, a);
+    }
+    if (eB == 5 && ltB == 8 && a.logC == 10 && a.logR >= 3 && !a.tq_b && a.pt) {
+        // past the four-step tables: persistent pass B (prefetches the next tile during this one)
+        static int cus = [] {
+            int dev = 0, n = 256;
+            if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+            return n;
         }();
-        // specialised tabled pass B (XFG_NTT_TQSPEC=0 disables, for A/B runs)
-        static const bool tqspec_on = [] {
-            const char* v = getenv("XFG_NTT_TQSPEC");
-            return !(v && *v == '0');
-        }();
-        // XFG_NTT_BPERS16: 0 = one tile per block at n = 2^16 (default), 1 / 2 = persistent with the
-        // table twiddles loaded per tile / prefetched (A/B knob)
-        static const int bpers16 = [] {
-            const char* v = getenv("XFG_NTT_BPERS16");
-            return v && *v ? atoi(v) : 0;
-        }();
-        int dev = 0, cus = 256;
-        auto ncu = [&] {
-            if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            return cus;
-        };
-        if (bpers_on && eB == 5 && ltB == 8 && a.logC == 10 && a.logR >= 3 && !a.tq_b && a.pt && !a.yblk) {
-            const int ntx = R >> logTR, ntiles = ntx * npoly * ncos;
-            const int nb = std::max(8, std::min(2 * ncu(), ntiles) & ~7);
-            hipLaunchKernelGGL((ntt_pass_b_pers<10, 8, 5, 0, 2>), dim3(nb), dim3(256), lds_b, s, a, ntx, ntiles);
-        } else if (!bpers16 && tqspec_on && eB == 4 && ltB == 8 && a.logC == 8 && a.logR >= 4 && a.t4 && a.tq_b && a.pt &&
-                   !a.yblk) {
-            static const size_t pad_b = (size_t)std::max(0, env_knob("XFG_NTT_BPAD", 0));  // occupancy probe
-            if (split_b) {
-                const size_t l = ((size_t)(1 << logTR) * row_pitch(C, 4, 4) * 4 + C * 8);
-                hipLaunchKernelGGL((ntt_pass_b_tq<8, 8, 4, true>), gb, dim3(256), l + pad_b, s, a);
-            } else
-                hipLaunchKernelGGL((ntt_pass_b_tq<8, 8, 4>), gb, dim3(256), lds_b + pad_b, s, a);  // lds_b < 64 KiB here
-        } else if (bpers16 && eB == 4 && ltB == 8 && a.logC == 8 && a.logR >= 4 && a.t4 && a.tq_b && a.pt) {
-            const int ntx = R >> logTR, ntiles = ntx * npoly * ncos;
-            if (bpers16 == 2) {
-                const int nb = std::max(8, std::min(3 * ncu(), ntiles) & ~7);
-                hipLaunchKernelGGL((ntt_pass_b_pers<8, 8, 4, 2, 3>), dim3(nb), dim3(256), lds_b, s, a, ntx, ntiles);
-            } else {
-                const int nb = std::max(8, std::min(4 * ncu(), ntiles) & ~7);
-                hipLaunchKernelGGL((ntt_pass_b_pers<8, 8, 4, 1, 4>), dim3(nb), dim3(256), lds_b, s, a, ntx, ntiles);
-            }
-        } else
-            run_pass_b<false>(a.logC, ltB, eB, gb, lds_b, s, a);
+        const int ntx = R >> logTR, ntiles = ntx * npoly * ncos;
+        const int nb = std::max(8, std::min(2 * cus, ntiles) & ~7);
+        hipLaunchKernelGGL((ntt_pass_b_pers<10, 8, 5, 2>), dim3(nb), dim3(256), lds_b, s, a, ntx, ntiles);
+    } else if (eB == 4 && ltB == 8 && a.logC == 8 && a.logR >= 4 && a.t4 && a.tq_b && a.pt) {
+        // the tabled LDE's pass B with the 32-bit split exchange (pass_dft_split): 19.5 instead of 37
+        // KiB of LDS per block, 6 instead of 4 waves per SIMD (pass B 919-942 vs 946-961 us per 64-proof
+        // launch set, same box)
+        const size_t l = ((size_t)(1 << logTR) * row_pitch(C, 4, 4) * 4 + C * 8);
+        hipLaunchKernelGGL((ntt_pass_b_tq<8, 8, 4>), gb, dim3(256), l, s, a);
+    } else {
+        run_pass_b<false>(a.logC, ltB, eB, gb, lds_b, s, a);
     }
 }
 
-// The four-step intermediate (beta * n per poly) is produced and consumed chunk by chunk so that
-// it stays resident in the 256 MiB Infinity Cache instead of round-tripping HBM.
-static int lde_chunk(int logn, int logbeta) {
-    const size_t per_poly = (size_t)8 << (logn + logbeta);
-    static const long mb = [] {
-        const char* v = getenv("XFG_LDE_CHUNK_MB");
-        return v && *v ? atol(v) : 0L;
-    }();
-    if (mb <= 0) return 1 << 30;  // no chunking
-    const size_t budget = (size_t)mb << 20;
-    size_t k = budget / per_poly;
-    return k < 1 ? 1 : (int)k;
-}
 void launch_lde(const u64* coef, u64 coef_stride, u64* out, u64* scratch, int npoly, int logn, int logbeta,
                 const Tables& T, hipStream_t s) {
-    const int chunk = lde_chunk(logn, logbeta);
-    const u64 N = 1ULL << (logn + logbeta);
-    for (int p0 = 0; p0 < npoly; p0 += chunk) {
-        NttArgs a{};
-        a.in = coef + (u64)p0 * coef_stride;
-        a.in_stride = coef_stride;
-        a.y = scratch;
-        a.out = out + (u64)p0 * N;
-        a.logn = logn;
-        a.logbeta = logbeta;
-        a.T = T;
-        a.t4 = (T.fs && logn <= FOURSTEP_MAX_LOG && logbeta <= 4) ? T.fs->fwd[logn][logbeta] : nullptr;
-        a.pt = a.t4 ? a.t4 + fourstep_main(logn, logbeta)
-                    : ((T.fs && logn <= PASS_MAX_LOG && logbeta <= 4) ? T.fs->pass_fwd[logn][logbeta] : nullptr);
-        ntt_run(a, std::min(chunk, npoly - p0), false, s);
-    }
+    NttArgs a{};
+    a.in = coef;
+    a.in_stride = coef_stride;
+    a.y = scratch;
+    a.out = out;
+    a.logn = logn;
+    a.logbeta = logbeta;
+    a.T = T;
+    a.t4 = (T.fs && logn <= FOURSTEP_MAX_LOG && logbeta <= 4) ? T.fs->fwd[logn][logbeta] : nullptr;
+    a.pt = a.t4 ? a.t4 + fourstep_main(logn, logbeta)
+                : ((T.fs && logn <= PASS_MAX_LOG && logbeta <= 4) ? T.fs->pass_fwd[logn][logbeta] : nullptr);
+    ntt_run(a, npoly, false, s);
 }
 
 void launch_interpolate(const u64* evals, u64 in_stride, u64* out, u64 out_stride, u64* scratch, int npoly, int logn,

@@ -416,16 +416,9 @@ static Tables tables_of(xfg_ctx* c) {
 // four-step twiddle tables of the NTT sizes one (n, beta) proof uses: the forward LDE and the
 // inverse NTTs of sizes 8 .. 2n (trace, composition, FRI remainder). Sizes whose table would exceed
 // 2^FOURSTEP_MAX_LOG entries keep the running-product twiddles. Returns false when one is missing.
-// largest log2(n beta) with a forward four-step table: FOURSTEP_MAX_LOG, or up to 24 with
-// XFG_FOURSTEP_MAX (A/B knob: configs[4]'s 2^24-point LDE with a 128 MiB table)
-static int fwd_table_max_log() {
-    static const int v = [] {
-        const char* e = getenv("XFG_FOURSTEP_MAX");
-        const int x = e && *e ? atoi(e) : FOURSTEP_MAX_LOG;
-        return std::min(std::max(x, FOURSTEP_MAX_LOG), 24);
-    }();
-    return v;
-}
+// largest log2(n beta) with a forward four-step table (a 2^24-entry table for configs[4] measured
+// slower than the running-product twiddles)
+static int fwd_table_max_log() { return FOURSTEP_MAX_LOG; }
 static bool fourstep_ready(xfg_ctx* c, int logn, int logbeta) {
     const FourStep& f = c->tables.fs;
     if (logn + logbeta <= fwd_table_max_log() && !f.fwd[logn][logbeta]) return false;
@@ -508,14 +501,12 @@ struct HostTrace {
     }
 };
 
-// the lane's stream for the openings' gathers: the highest stream priority unless XFG_GATHER_PRIO=0
-// (then the default priority, still a stream of its own)
-static int env_int(const char* name, int dflt);
+// the lane's stream for the openings' gathers, at the highest stream priority (a second stream at
+// the default priority measured 4-5 % slower)
 static hipStream_t gather_stream(Lane* c) {
     if (!c->gstream) {
-        static const int on = env_int("XFG_GATHER_PRIO", 1);
         int least = 0, greatest = 0;
-        if (!on || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
+        if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
         HIPCHK(hipStreamCreateWithPriority(&c->gstream, hipStreamNonBlocking, greatest));
     }
     return c->gstream;
@@ -1074,23 +1065,13 @@ static Lane* lane0(xfg_ctx* c) {
     }
     return c->lanes[0].get();
 }
-// XFG_LANE_PRIO (A/B knob): 1 = the first XFG_PRIO_HIGH lanes (default 3) on high-priority streams,
-// 2 = priorities graded by lane index; 0 (default) = every lane at the default priority
-static int lane_priority(int l) {
-    static const int mode = env_int("XFG_LANE_PRIO", 0), high = env_int("XFG_PRIO_HIGH", 3);
-    int least = 0, greatest = 0;
-    if (!mode || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return 0;
-    if (mode == 1) return l < high ? greatest : least;
-    const int span = least - greatest;  // greatest is numerically smaller
-    return std::max(greatest, least - (span ? l % (span + 1) : 0));
-}
 static void ensure_lanes(xfg_ctx* c, size_t k) {
     lane0(c);
     while (c->lanes.size() < k) {
         c->lanes.emplace_back(new Lane());
         c->lanes.back()->lde_probe = c->lde_probe;
-        HIPCHK(hipStreamCreateWithPriority(&c->lanes.back()->stream, hipStreamNonBlocking,
-                                           lane_priority((int)c->lanes.size() - 1)));
+        // every lane at the default priority (graded or high lane priorities measured equal or worse)
+        HIPCHK(hipStreamCreateWithFlags(&c->lanes.back()->stream, hipStreamNonBlocking));
         for (auto& e : c->lanes.back()->ev) HIPCHK(hipEventCreate(&e));
     }
 }
@@ -1392,16 +1373,35 @@ int xfg_last_error(const xfg_ctx* c, char* buf, size_t len) {
     return (int)c->err.size();
 }
 
+// Bytes of one serialised batch opening of `nu` leaves of an L-leaf tree (the u32 length, the u8
+// vector count, one u8 length per vector, the digests): plan_batch_opening emits at most one node per
+// distinct tree node at each level, so level j (2^j nodes) contributes at most min(nu, 2^j) digests.
+static size_t opening_bound(u64 L, u64 nu) {
+    size_t s = 4 + 1 + nu;
+    for (unsigned j = 1; j <= ilog2(L); j++) s += 32 * std::min<u64>(nu, 1ULL << j);
+    return s;
+}
+
+// The largest StarkProof::to_bytes this prover emits for (n, options), section by section as the
+// serialiser below writes them, with nu = min(q, N) unique queries. Tight (configs[2]: 98.8 KB
+// against ~78 KB proofs), so a fixed-size exchange record per proof costs little (bench.py).
 size_t xfg_proof_size_bound(uint64_t n, const xfg_options* opts) {
     if (!opts || !is_pow2(n)) return 0;
     Opts o = to_opts(opts);
-    u64 N = n * o.beta, depth = ilog2(N);
-    unsigned L = num_fri_layers(N, o);
+    if (o.fold < 2 || !is_pow2(o.fold) || o.beta == 0 || !is_pow2(o.beta)) return 0;
+    const u64 N = n * o.beta, nu = std::min<u64>(o.q, N);
+    const unsigned nl = num_fri_layers(N, o), lf = ilog2(o.fold);
     const size_t de = o.ext == 2 ? 2 : 1;
-    size_t s = 4096 + o.q * (7 * 8 + 8 * de + (size_t)L * o.fold * 8 * de);
-    s += (size_t)(2 + L) * (1 + o.q * (1 + depth * 32));
-    s += (size_t)N * 8 * de / o.beta + 32 * (L + 3);
-    return s;
+    const u64 rem_len = std::max<u64>(N >> (lf * nl) >> ilog2(o.beta), 1);
+    size_t s = 7 + 9 + 6 + 1;                            // Context, num_unique_queries
+    s += 2 + 32 * (size_t)(3 + nl);                      // commitments: trace, composition, layers, remainder
+    s += 1 + 4 + nu * 7 * 8 + opening_bound(N, nu);      // trace queries
+    s += 4 + nu * 8 * de + opening_bound(N, nu);         // constraint queries
+    s += 2 + 1 + 14 * 8 * de + 2 + 8 * de;               // OOD frame
+    s += 1;                                              // FRI layer count
+    for (unsigned l = 0; l < nl; l++) s += 4 + nu * o.fold * 8 * de + opening_bound(N >> (lf * (l + 1)), nu);
+    s += 2 + rem_len * 8 * de + 1 + 8;                   // remainder, partitions, pow nonce
+    return s + 64;
 }
 
 int xfg_burn_air_consts(const xfg_burn_inputs* in, xfg_air_consts* out) {

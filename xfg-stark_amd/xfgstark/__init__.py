@@ -342,13 +342,29 @@ def _anon_map(size):
     return mmap.mmap(-1, size, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
 
 
-class PendingBatch:
-    """a submitted batch (XfgBurnMintProver.submit_batch); result() -> list of StarkProof | XfgStarkError"""
+def record_size(count, trace_length, options):
+    """bytes of a fixed-size batch record (XfgBurnMintProver.submit_batch_record): `count` int64
+    proof lengths, then `count` slots of xfg_proof_size_bound bytes, proof i at slot i"""
+    o = options._c()
+    return 8 * count + count * _lib.xfg_proof_size_bound(trace_length, C.byref(o))
 
-    def __init__(self, prover, ticket, buf, base, cap, outs, lens, sts):
+
+class PendingBatch:
+    """a submitted batch (XfgBurnMintProver.submit_batch); result() -> list of StarkProof | XfgStarkError.
+    A batch is consumed once: by result() (which can be called again and returns the same list),
+    by packed_into(), or -- for a batch written into a caller's record -- by record_ready()."""
+
+    def __init__(self, prover, ticket, buf, base, cap, outs, lens, sts, record=False):
         self._p, self._t, self._buf, self._base, self._cap = prover, ticket, buf, base, cap
         self._outs, self._lens, self._sts = outs, lens, sts
+        self._record = record  # proofs live in the caller's record: no pooled buffer to release
         self._res = None
+        self._consumed = None  # name of the call that consumed the batch, if not result()
+
+    def _release(self):
+        if self._buf is not None:
+            self._p._free.append(self._buf)
+            self._buf = None
 
     def wait(self):
         """block until every proof of the batch is done (idempotent); the batch's status code"""
@@ -356,11 +372,16 @@ class PendingBatch:
             self._wst = _lib.xfg_batch_wait(self._p._ctx, self._t)
         return self._wst
 
+    def _check_unconsumed(self, what):
+        if self._consumed:
+            raise XfgStarkError(9, f"{what} after {self._consumed}(): the batch was already consumed")
+
     def result(self):
         if self._res is None:
+            self._check_unconsumed("result")
             st = self.wait()
             if st:
-                self._p._free.append(self._buf)
+                self._release()
                 raise self._p._err(st)
             res = []
             for i in range(len(self._sts)):
@@ -368,47 +389,68 @@ class PendingBatch:
                     res.append(XfgStarkError(self._sts[i], STATUS.get(self._sts[i])))
                 else:
                     res.append(StarkProof(C.string_at(self._base + i * self._cap, self._lens[i])))
-            self._p._free.append(self._buf)
+            self._release()
             self._res = res
         return self._res
 
+    def record_ready(self):
+        """wait for a batch submitted with submit_batch_record; its record (lengths + fixed slots)
+        is then complete in the caller's buffer. A failed proof raises (its length is zeroed in the
+        record first, so a record that travels anyway cannot be read as a proof)."""
+        if not self._record:
+            raise XfgStarkError(9, "record_ready: the batch was not submitted into a record")
+        self._check_unconsumed("record_ready")
+        if self._res is not None:
+            raise XfgStarkError(9, "record_ready after result()")
+        self._consumed = "record_ready"
+        st = self.wait()
+        bad = [i for i in range(len(self._sts)) if self._sts[i]]
+        for i in bad:
+            self._lens[i] = 0
+        if st:
+            raise self._p._err(st)
+        if bad:
+            raise XfgStarkError(self._sts[bad[0]], STATUS.get(self._sts[bad[0]]))
+        return 8 * len(self._sts) + self._cap * len(self._sts)
+
     def packed_into(self, dst):
         """wait, then write the batch as one record into the uint8 numpy array `dst`: count int64
-        lengths followed by the proof bytes back to back (the exchange format of a sharded run,
-        bench.gather_proofs), straight from the workers' output buffer -- no per-proof bytes
-        objects. Returns the record size. Any per-proof error raises."""
+        lengths followed by the proof bytes back to back, straight from the workers' output buffer
+        -- no per-proof bytes objects. Returns the record size. Any per-proof error raises."""
         import numpy as np
-        if self._res is None:
-            st = self.wait()
-            if st:
-                self._p._free.append(self._buf)
-                self._res = []
-                raise self._p._err(st)
-            k = len(self._sts)
-            bad = [i for i in range(k) if self._sts[i]]
-            lens = np.array([self._lens[i] for i in range(k)], dtype=np.int64)
-            hdr = 8 * k
-            need = hdr + int(lens.sum())
-            if bad or need > dst.size:
-                self._p._free.append(self._buf)
-                self._res = []
-                if bad:
-                    raise XfgStarkError(self._sts[bad[0]], STATUS.get(self._sts[bad[0]]))
-                raise XfgStarkError(8, "packed_into: destination too small")
-            dst[:hdr] = lens.view(np.uint8)
-            base, off = dst.ctypes.data, hdr
-            for i in range(k):
-                C.memmove(base + off, self._base + i * self._cap, int(lens[i]))
-                off += int(lens[i])
-            self._p._free.append(self._buf)
-            self._res = []  # consumed: result() is not available after packed_into
-            return need
-        raise XfgStarkError(9, "packed_into after result(): the batch's buffer was released")
+        if self._res is not None:
+            raise XfgStarkError(9, "packed_into after result(): the batch's buffer was released")
+        self._check_unconsumed("packed_into")
+        self._consumed = "packed_into"
+        st = self.wait()
+        if st:
+            self._release()
+            raise self._p._err(st)
+        k = len(self._sts)
+        bad = [i for i in range(k) if self._sts[i]]
+        lens = np.array([self._lens[i] for i in range(k)], dtype=np.int64)
+        hdr = 8 * k
+        need = hdr + int(lens.sum())
+        if bad or need > dst.size:
+            self._release()
+            if bad:
+                raise XfgStarkError(self._sts[bad[0]], STATUS.get(self._sts[bad[0]]))
+            raise XfgStarkError(8, "packed_into: destination too small")
+        dst[:hdr] = lens.view(np.uint8)
+        base, off = dst.ctypes.data, hdr
+        for i in range(k):
+            C.memmove(base + off, self._base + i * self._cap, int(lens[i]))
+            off += int(lens[i])
+        self._release()
+        return need
 
     def __del__(self):
-        # the workers write into this batch's buffers: never release them before the batch is done
-        if self._res is None and getattr(self._p, "_ctx", None):
-            _lib.xfg_batch_wait(self._p._ctx, self._t)
+        # the workers write into this batch's buffers: never release them before the batch is done;
+        # a batch that was waited for but never consumed returns its buffer to the pool
+        if getattr(self._p, "_ctx", None):
+            if self._res is None and not hasattr(self, "_wst"):
+                _lib.xfg_batch_wait(self._p._ctx, self._t)
+            self._release()
 
 
 class XfgBurnMintProver:
@@ -450,6 +492,11 @@ class XfgBurnMintProver:
 
     def get_proof_size(self, proof: StarkProof) -> int:
         return len(proof.to_bytes())
+
+    def proof_size_bound(self, trace_length) -> int:
+        """the largest proof this prover emits for `trace_length` under its options (xfg_proof_size_bound)"""
+        o = self._options._c()
+        return _lib.xfg_proof_size_bound(trace_length, C.byref(o))
 
     def prove_burn_mint(self, burn_amount, mint_amount, tx_prefix_hash, recipient_address, secret, network_id=1,
                         target_chain_id=42161, commitment_version=1, trace_length=64) -> StarkProof:
@@ -512,6 +559,35 @@ class XfgBurnMintProver:
             self._free.append(buf)
             raise self._err(st)
         return PendingBatch(self, ticket.value, buf, base, cap, outs, lens, sts)
+
+    def submit_batch_record(self, inputs, trace_length, addr, nbytes):
+        """submit_batch whose output is a caller-owned fixed-size record at host address `addr`
+        (record_size bytes): the workers write proof i into slot i and its length into header word
+        i, so the record can be handed to a collective (bench.py's exchange step) without packing.
+        The record must stay valid and untouched until PendingBatch.record_ready() returns."""
+        k = len(inputs)
+        o = self._options._c()
+        cap = _lib.xfg_proof_size_bound(trace_length, C.byref(o))
+        if k == 0 or cap == 0 or nbytes < 8 * k + cap * k:
+            raise XfgStarkError(9, f"submit_batch_record: record of {nbytes} B for {k} proofs of bound {cap} B")
+        arr = (_BurnInputs * k)()
+        keep = []
+        for i, kw in enumerate(inputs):
+            s = burn_inputs(**kw)
+            keep.append(s._keep)
+            arr[i] = s
+        base = addr + 8 * k
+        outs = (_u8p * k)(*[C.cast(base + i * cap, _u8p) for i in range(k)])
+        lens = (C.c_size_t * k).from_address(addr)  # the record's header: capacity in, length out
+        for i in range(k):
+            lens[i] = cap
+        sts = (C.c_int * k)()
+        ticket = C.c_uint64(0)
+        st = _lib.xfg_prove_batch_submit(self._ctx, k, arr, trace_length, C.byref(o), outs, lens, sts,
+                                         C.byref(ticket))
+        if st:
+            raise self._err(st)
+        return PendingBatch(self, ticket.value, None, base, cap, outs, lens, sts, record=True)
 
     def _take_buffer(self, size):
         # output buffers are recycled. A new one is an anonymous mapping, not create_string_buffer:
