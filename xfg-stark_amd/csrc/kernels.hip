@@ -951,14 +951,6 @@ void launch_coin_draw_test(const DevCoin& c0, int k, int ext, const u64* rej, u6
 }
 
 // ============================================================================ gathers
-__global__ void gather_u64_kernel(const u64* src, const u64* idx, u64* dst, u64 count) {
-    u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < count) dst[i] = src[idx[i]];
-}
-__global__ void gather_digest_kernel(const Digest* src, const u64* idx, Digest* dst, u64 count) {
-    u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < count) dst[i] = src[idx[i]];
-}
 // all of a unit's opening gathers in one launch: thread i of the grid serves element i - first[k] of
 // segment k (the segments are laid end to end in index order; at most GatherSet::MAX of them)
 __global__ void gather_set_kernel(GatherSet g, const u64* idx) {
@@ -979,15 +971,6 @@ void launch_gather_set(const GatherSet& g, const u64* idx, hipStream_t s) {
     if (!total) return;
     hipLaunchKernelGGL(gather_set_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, g, idx);
     XFG_CHECK_LAUNCH();
-}
-void launch_gather_u64(const u64* src, const u64* idx, u64* dst, u64 count, hipStream_t s) {
-    if (!count) return;
-    hipLaunchKernelGGL(gather_u64_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s, src, idx, dst, count);
-}
-void launch_gather_digest(const Digest* src, const u64* idx, Digest* dst, u64 count, hipStream_t s) {
-    if (!count) return;
-    hipLaunchKernelGGL(gather_digest_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s, src, idx, dst,
-                       count);
 }
 
 }  // namespace xfg

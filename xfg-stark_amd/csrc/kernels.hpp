@@ -149,7 +149,6 @@ void launch_fri_fold(const u64* vals, u64 val_stride, u64 comp_stride, bool cose
                      int ext, hipStream_t s);
 
 // ---- openings ----
-void launch_gather_u64(const u64* src, const u64* idx, u64* dst, u64 count, hipStream_t s);
 // several gathers in one launch: segment k copies src[k][idx[first[k] + j]] to dst[k][j],
 // j < first[k + 1] - first[k], as u64 or as Digest (digest[k])
 struct GatherSet {
@@ -161,6 +160,5 @@ struct GatherSet {
     u64 first[MAX + 1] = {0};
 };
 void launch_gather_set(const GatherSet& g, const u64* idx, hipStream_t s);
-void launch_gather_digest(const Digest* src, const u64* idx, Digest* dst, u64 count, hipStream_t s);
 
 }  // namespace xfg

@@ -247,7 +247,8 @@ struct NttArgs {
     u64 keep;     // inverse: coefficients written
     const u64* t4;  // four-step twiddle table (FourStep) or nullptr
     const u64* pt;  // pass tables: w_R^(+-i) [R], w_C^(+-i) [C], forward coset pre-factors [beta][R]; or nullptr
-    int xcd;        // 1: XCD-contiguous block order (see xcd_block)
+    int xcd;        // 1 / 2: XCD-contiguous block order of pass A / B (xcd_block); 4: pass A cosets
+                    // of a tile consecutive (xcd_block_coset)
     int tq_b;       // forward: pass B applies the four-step twiddles as it loads (ntt_pass_a_cos)
     int preg;       // forward pass A: coset pre-factors read from the pass tables in L2, not LDS
     Tables T;
@@ -270,6 +271,20 @@ __device__ __forceinline__ void xcd_block(bool on, int& bx, int& by) {
     by = l / gridDim.x;
 }
 
+// The same XCD-contiguous renumbering with the cosets of a (poly, column tile) consecutive: the
+// beta blocks that read one coefficient tile then run side by side on one XCD, so the tile comes
+// from HBM once and from that XCD's L2 beta - 1 times (forward pass A without the all-coset kernel:
+// configs[4]'s R = 1024); the two 64 B halves of an intermediate line (tiles 2i, 2i + 1 of a coset)
+// are written 2^logbeta blocks apart on the same XCD.
+__device__ __forceinline__ void xcd_block_coset(int logbeta, int& bx, int& by) {
+    const int total = gridDim.x * gridDim.y, L = blockIdx.x + gridDim.x * blockIdx.y;
+    const int per = total >> 3, rem = total & 7, x = L & 7, slot = L >> 3;
+    const int l = (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + slot;
+    const int t = l & ((1 << logbeta) - 1), rest = l >> logbeta;
+    bx = rest % gridDim.x;
+    by = ((rest / gridDim.x) << logbeta) + t;
+}
+
 // ---------------------------------------------------------------- pass A: column DFTs (size R)
 // forward, coset t: x[j1] = c[C j1 + j2] * 7^(C j1) w_(beta R)^(t j1)
 //   y[t][k1][j2] = X[k1] * 7^j2 * w_N^(j2 (t + beta k1))
@@ -289,7 +304,8 @@ __global__ __launch_bounds__(1 << LOGT, (1 << (10 - LOGT)) >> (LOGE - 4)) void n
     u64* pre = ltw + R;  // forward: 7^(C j1) w_(beta R)^(t j1) for this block's coset
     // one block per (column tile, poly, coset); y is [poly][coset][R][C]
     int bx, by;
-    xcd_block(a.xcd & 1, bx, by);
+    if (!INV && (a.xcd & 4)) xcd_block_coset(a.logbeta, bx, by);
+    else xcd_block(a.xcd & 1, bx, by);
     const int pt = by, col0 = bx * TC;
     const int poly = INV ? pt : (pt >> a.logbeta), t = INV ? 0 : (pt & ((1 << a.logbeta) - 1));
     const u64 n = 1ULL << a.logn;
@@ -890,7 +906,7 @@ static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
     dim3 ga(C >> logTC, npoly * ncos), gb(R >> logTR, npoly * ncos);
     // XCD-contiguous block order where a tile row of the scattered writes is narrower than a 128 B
     // line: pass A stores TC consecutive words per row, pass B TR (xcd_block)
-    a.xcd = (logTC < 4 ? 1 : 0) | (logTR < 4 ? 2 : 0);
+    a.xcd = (logTC < 4 ? 1 : 0) | (logTR < 4 ? 2 : 0) | (a.preg ? 4 : 0);
     if (inv) {
         run_pass_a<true>(a.logR, ltA, eA, ga, lds_a, s, a);
         run_pass_b<true>(a.logC, ltB, eB, gb, lds_b, s, a);

@@ -363,7 +363,6 @@ struct xfg_ctx {
         xfg::HBuf<uint8_t> stage;  // pinned: proof blob + task lists, one DMA
         xfg::DBuf<uint8_t> dstage;
         xfg::DBuf<uint32_t> flags;
-        xfg::DBuf<xfg::Digest> dig, rootdig;
         std::vector<xfg::VState> st;        // per-proof transcript states, reused between calls
         std::vector<xfg::VerifyPlan> frag;  // per-proof plan fragments, reused between calls
     } vb;
@@ -1890,13 +1889,12 @@ int xfg_verify_batch_gpu(xfg_ctx* c, uint32_t count, const uint8_t* const* proof
             }
         });
         ht.mark("transcripts");
-        // 2. plan: per-proof task fragments (local slot numbers) built in parallel; blob offsets by
-        //    prefix sum of the accepted proofs' lengths
+        // 2. plan: per-proof fragments (openings, queries) built in parallel; blob offsets by prefix
+        //    sum of the accepted proofs' lengths
         std::vector<size_t> boff(count + 1, 0);
         for (uint32_t i = 0; i < count; i++) boff[i + 1] = boff[i] + (err[i].empty() ? lens[i] : 0);
         std::vector<VerifyPlan>& frag = V.frag;
         parallel([&](uint32_t i) {
-            reset_plan(frag[i]);
             if (!err[i].empty()) return;
             std::string e;
             if (!plan_proof(st[i], boff[i], frag[i], e)) err[i] = e;
@@ -1904,109 +1902,72 @@ int xfg_verify_batch_gpu(xfg_ctx* c, uint32_t count, const uint8_t* const* proof
         ht.mark("plan_fragments");
         // 3. concatenate into one pinned staging region (parallel fill) and one DMA
         struct Off {
-            size_t slot = 0, g = 0, lv = 0, q = 0, fp = 0, root = 0;
-            std::vector<size_t> r;
+            size_t t = 0, lf = 0, v = 0, q = 0, fp = 0;
         };
         std::vector<Off> fo(count + 1);
-        size_t nrounds = 0;
-        for (uint32_t i = 0; i < count; i++)
-            if (err[i].empty()) nrounds = std::max(nrounds, frag[i].rounds.size());
-        std::vector<std::vector<size_t>> rcount(nrounds, std::vector<size_t>(count + 1, 0));
         std::vector<int> planned(count, -1);
-        int nplanned = 0;
         for (uint32_t i = 0; i < count; i++) {
             const bool ok = err[i].empty();
             const VerifyPlan& f = frag[i];
             Off& a = fo[i];
             Off& b = fo[i + 1];
-            b.slot = a.slot + (ok ? f.nslots : 0);
-            b.g = a.g + (ok ? f.gathers.size() : 0);
-            b.lv = a.lv + (ok ? f.leaves.size() : 0);
+            b.t = a.t + (ok ? f.trees.size() : 0);
+            b.lf = a.lf + (ok ? f.tleaves.size() : 0);
+            b.v = a.v + (ok ? f.vecs.size() : 0);
             b.q = a.q + (ok ? f.fqueries.size() : 0);
             b.fp = a.fp + (ok ? 1 : 0);
-            b.root = a.root + (ok ? f.roots[0].size() : 0);
-            for (size_t r = 0; r < nrounds; r++)
-                rcount[r][i + 1] = rcount[r][i] + (ok && r < f.rounds.size() ? f.rounds[r].size() : 0);
-            if (ok) planned[i] = nplanned++;
+            if (ok) planned[i] = (int)a.fp;
         }
-        std::vector<size_t> rbase(nrounds + 1, 0);
-        for (size_t r = 0; r < nrounds; r++) rbase[r + 1] = rbase[r] + rcount[r][count];
+        const Off& E = fo[count];
         auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-        const size_t o_blob = 0, o_g = al(boff[count]), o_lv = al(o_g + fo[count].g * sizeof(VGather)),
-                     o_r = al(o_lv + fo[count].lv * sizeof(VLeaf)), o_fp = al(o_r + rbase[nrounds] * 4),
-                     o_fq = al(o_fp + fo[count].fp * sizeof(VFieldProof)),
-                     o_ri = al(o_fq + fo[count].q * sizeof(VFieldQuery)), total_b = al(o_ri + fo[count].root * 8);
+        const size_t o_blob = 0, o_t = al(boff[count]), o_lf = al(o_t + E.t * sizeof(VTree)),
+                     o_v = al(o_lf + E.lf * sizeof(VTreeLeaf)), o_fp = al(o_v + E.v * sizeof(VVec)),
+                     o_fq = al(o_fp + E.fp * sizeof(VFieldProof)), total_b = al(o_fq + E.q * sizeof(VFieldQuery));
         uint8_t* H = V.stage.ensure(total_b);
-        VGather* hg = (VGather*)(H + o_g);
-        VLeaf* hl = (VLeaf*)(H + o_lv);
-        uint32_t* hr = (uint32_t*)(H + o_r);
+        VTree* ht_ = (VTree*)(H + o_t);
+        VTreeLeaf* hlf = (VTreeLeaf*)(H + o_lf);
+        VVec* hv = (VVec*)(H + o_v);
         VFieldProof* hfp = (VFieldProof*)(H + o_fp);
         VFieldQuery* hfq = (VFieldQuery*)(H + o_fq);
-        u64* hri = (u64*)(H + o_ri);
-        std::vector<int64_t> rootslot(fo[count].root);
         parallel([&](uint32_t i) {
-            if (boff[i + 1] > boff[i]) memcpy(H + o_blob + boff[i], proofs[i], lens[i]);
             if (planned[i] < 0) return;
+            memcpy(H + o_blob + boff[i], proofs[i], lens[i]);
             const VerifyPlan& f = frag[i];
             const Off& a = fo[i];
-            const uint32_t sb = (uint32_t)a.slot;
-            for (size_t k = 0; k < f.gathers.size(); k++) {
-                hg[a.g + k] = f.gathers[k];
-                hg[a.g + k].dst += sb;
+            for (size_t k = 0; k < f.trees.size(); k++) {
+                VTree t = f.trees[k];
+                t.leaf0 += (uint32_t)a.lf;
+                t.vec0 += (uint32_t)a.v;
+                t.proof = (uint32_t)a.fp;
+                ht_[a.t + k] = t;
             }
-            for (size_t k = 0; k < f.leaves.size(); k++) {
-                hl[a.lv + k] = f.leaves[k];
-                hl[a.lv + k].dst += sb;
-            }
-            for (size_t r = 0; r < f.rounds.size(); r++) {
-                uint32_t* d = hr + rbase[r] + rcount[r][i];
-                for (size_t k = 0; k < f.rounds[r].size(); k++) d[k] = f.rounds[r][k] + sb;
-            }
-            hfp[a.fp] = f.fproofs[0];
+            memcpy(hlf + a.lf, f.tleaves.data(), f.tleaves.size() * sizeof(VTreeLeaf));
+            memcpy(hv + a.v, f.vecs.data(), f.vecs.size() * sizeof(VVec));
+            hfp[a.fp] = f.fproof;
             for (size_t k = 0; k < f.fqueries.size(); k++) {
                 hfq[a.q + k] = f.fqueries[k];
                 hfq[a.q + k].proof = (uint32_t)a.fp;
             }
-            for (size_t t = 0; t < f.roots[0].size(); t++) {
-                const int64_t r = f.roots[0][t];
-                rootslot[a.root + t] = r >= 0 ? r + sb : -1;
-                hri[a.root + t] = r >= 0 ? (u64)(r + sb) : 0;
-            }
         });
         ht.mark("plan_merge");
-        std::vector<Digest> rootd(fo[count].root);
-        std::vector<uint32_t> flags(fo[count].fp, 0);
-        if (nplanned > 0) {
+        std::vector<uint32_t> flags(E.fp, 0);
+        if (E.fp > 0) {
             hipStream_t s = lane0(c)->stream;
             V.dstage.ensure(total_b);
-            V.dig.ensure(std::max<size_t>(1, fo[count].slot));
-            V.flags.ensure(fo[count].fp);
-            V.rootdig.ensure(fo[count].root);
+            V.flags.ensure(E.fp);
             HIPCHK(hipMemcpyAsync(V.dstage.p, H, total_b, hipMemcpyHostToDevice, s));
-            HIPCHK(hipMemsetAsync(V.flags.p, 0, fo[count].fp * 4, s));
+            HIPCHK(hipMemsetAsync(V.flags.p, 0, E.fp * 4, s));
             ht.mark("upload_enqueue");
             uint8_t* D = V.dstage.p;
-            launch_verify(D + o_blob, (const VGather*)(D + o_g), fo[count].g, (const VLeaf*)(D + o_lv), fo[count].lv,
-                          (const uint32_t*)(D + o_r), rbase.data(), (int)nrounds, (const VFieldProof*)(D + o_fp),
-                          (const VFieldQuery*)(D + o_fq), fo[count].q, V.dig.p, V.flags.p, s);
-            launch_gather_digest(V.dig.p, (const u64*)(D + o_ri), V.rootdig.p, fo[count].root, s);
-            HIPCHK(hipMemcpyAsync(rootd.data(), V.rootdig.p, rootd.size() * sizeof(Digest), hipMemcpyDeviceToHost, s));
+            launch_verify(D + o_blob, (const VTree*)(D + o_t), E.t, (const VTreeLeaf*)(D + o_lf), (const VVec*)(D + o_v),
+                          (const VFieldProof*)(D + o_fp), (const VFieldQuery*)(D + o_fq), E.q, V.flags.p, s);
             HIPCHK(hipMemcpyAsync(flags.data(), V.flags.p, flags.size() * 4, hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));
             ht.mark("device");
         }
         // 4. verdicts in the host verifier's check order
         parallel([&](uint32_t i) {
-            if (planned[i] >= 0) {
-                const Off& a = fo[i];
-                const size_t nr = fo[i + 1].root - a.root;
-                std::vector<Digest> rd(nr);
-                for (size_t t = 0; t < nr; t++) {
-                    if (rootslot[a.root + t] >= 0) rd[t] = rootd[a.root + t];
-                    else memset(rd[t].w, 0xFF, 32);
-                }
-                err[i] = finish_proof(st[i], rd, flags[a.fp]);
-            }
+            if (planned[i] >= 0) err[i] = finish_proof(st[i], flags[planned[i]]);
             results[i] = proofs[i] ? (err[i].empty() ? XFG_OK : XFG_VERIFY_FAILED) : XFG_INVALID_ARGUMENT;
         });
         ht.mark("finish");

@@ -98,6 +98,7 @@ std::string parse_proof(const uint8_t* bytes, size_t len, ParsedProof& pf) {
     const uint8_t* c = r.take(clen);
     if (!c || clen % 32) return "ProofDeserializationError(\"commitments\")";
     pf.com.resize(clen / 32);
+    pf.com_p = c;
     if (clen) memcpy(pf.com.data(), c, clen);  // (an empty vector's data() may be null)
     if (r.u(1) != 1) return "ProofDeserializationError(\"trace queries: expected one segment\")";
     if (!read_span(r, 4, pf.trace_rows)) return "ProofDeserializationError(\"trace queries\")";
@@ -471,41 +472,35 @@ static std::string verify_proof(const uint8_t* bytes, size_t len, const AirConst
 }
 
 // ------------------------------------------------------------------ batched GPU verification plan
-void reset_plan(VerifyPlan& plan) {
-    plan.blob.clear();
-    plan.gathers.clear();
-    plan.leaves.clear();
-    for (auto& r : plan.rounds) r.clear();
-    plan.fproofs.clear();
-    plan.fqueries.clear();
-    plan.nslots = 0;
-    plan.roots.clear();
-    plan.fidx.clear();
-}
 bool plan_proof(const VState& st, size_t blob_off, VerifyPlan& plan, std::string& err) {
     const ParsedProof& pf = st.pf;
     const int de = st.de;
     const u64 N = st.N, nu = pf.num_unique;
     const unsigned nl = st.nl;
+    plan.trees.clear();
+    plan.tleaves.clear();
+    plan.vecs.clear();
+    plan.fqueries.clear();
     if (nl > (unsigned)VMAXL) {
         err = "ProofDeserializationError(\"too many FRI layers\")";
         return false;
     }
     auto off = [&](const uint8_t* p) { return (u64)blob_off + (u64)(p - pf.base); };
-    // FRI position lists and the structural checks of the host verifier
+    // FRI position lists (first-occurrence order, the order of the opened rows) and the structural
+    // checks the host verifier makes before it opens anything
     thread_local std::vector<std::vector<u64>> fps;
     fps.resize(nl);
     {
-        std::vector<u64> cur = st.pos;
+        const std::vector<u64>* cur = &st.pos;
         u64 D = N;
         for (unsigned l = 0; l < nl; l++) {
             const u64 rows = D / 8;
-            fps[l] = fold_positions(cur, rows);
+            fps[l] = fold_positions(*cur, rows);
             if (pf.fri_vals[l].n != fps[l].size() * 64 * de) {
                 err = "FriVerificationFailed(InvalidLayerCommitment)";
                 return false;
             }
-            cur = fps[l];
+            cur = &fps[l];
             D = rows;
         }
         const u64 rl = pf.fri_rem.n / (8 * de);
@@ -514,35 +509,36 @@ bool plan_proof(const VState& st, size_t blob_off, VerifyPlan& plan, std::string
             return false;
         }
     }
-    // Merkle trees: leaves, given nodes, merges by level -> digest slots
-    plan.roots.emplace_back();
-    std::vector<int64_t>& roots = plan.roots.back();
-    auto add_tree = [&](const std::vector<u64>& idx, const Paths& paths, u64 L, const uint8_t* leaf0, size_t stride,
-                        uint32_t words) -> int64_t {
-        thread_local MerkleSym sym;
-        if (!merkle_symbolic(idx, paths, L, sym)) return -1;
-        const uint32_t b = plan.nslots;
-        for (size_t i = 0; i < idx.size(); i++)
-            plan.leaves.push_back(VLeaf{off(leaf0 + i * stride), words, b + sym.leaf_slot[i]});
-        for (auto& g : sym.given) plan.gathers.push_back(VGather{off(g.second), b + g.first, 0});
-        if (plan.rounds.size() < sym.nlev) plan.rounds.resize(sym.nlev);
-        for (size_t r = 0; r < sym.nlev; r++)
-            for (uint32_t x : sym.levels[r]) plan.rounds[r].push_back(b + x);
-        plan.nslots += sym.nslots;
-        return (int64_t)(b + sym.root);
+    // one VTree per batch opening: the opened rows sorted by leaf index, the node vectors as the
+    // proof holds them; the device checks that they fit the opening (BatchMerkleProof::get_root)
+    auto add_tree = [&](const u64* idx, size_t cnt, const Paths& paths, unsigned depth, const uint8_t* row0,
+                        size_t stride, uint32_t words, unsigned com, uint32_t bit) {
+        VTree t{};
+        t.root_off = off(pf.com_p + 32 * com);
+        t.leaf0 = (uint32_t)plan.tleaves.size();
+        t.nidx = (uint32_t)cnt;
+        t.vec0 = (uint32_t)plan.vecs.size();
+        t.nvec = (uint32_t)paths.ptr.size();
+        t.words = words;
+        t.depth = depth;
+        t.bit = bit;
+        const size_t l0 = plan.tleaves.size();
+        for (size_t i = 0; i < cnt; i++) plan.tleaves.push_back(VTreeLeaf{idx[i], off(row0 + i * stride)});
+        std::sort(plan.tleaves.begin() + l0, plan.tleaves.end(),
+                  [](const VTreeLeaf& x, const VTreeLeaf& y) { return x.index < y.index; });
+        for (size_t v = 0; v < paths.ptr.size(); v++) plan.vecs.push_back(VVec{off(paths.ptr[v]), paths.cnt[v], 0});
+        plan.trees.push_back(t);
     };
-    roots.push_back(add_tree(st.pos, pf.trace_paths, N, pf.trace_rows.p, 56, 7));
-    roots.push_back(add_tree(st.pos, pf.constraint_paths, N, pf.constraint_rows.p, 8 * de, (uint32_t)de));
-    {
-        u64 D = N;
-        for (unsigned l = 0; l < nl; l++) {
-            const u64 rows = D / 8;
-            roots.push_back(add_tree(fps[l], pf.fri_paths[l], rows, pf.fri_vals[l].p, 64 * de, (uint32_t)(8 * de)));
-            D = rows;
-        }
-    }
+    const unsigned depthN = ilog2(N);
+    add_tree(st.pos.data(), nu, pf.trace_paths, depthN, pf.trace_rows.p, 56, 7, 0, VF_TRACE);
+    add_tree(st.pos.data(), nu, pf.constraint_paths, depthN, pf.constraint_rows.p, 8 * de, (uint32_t)de, 1,
+             VF_CONSTRAINT);
+    for (unsigned l = 0; l < nl; l++)
+        add_tree(fps[l].data(), fps[l].size(), pf.fri_paths[l], depthN - 3 * (l + 1), pf.fri_vals[l].p, 64 * de,
+                 (uint32_t)(8 * de), 2 + l, 1u << (VF_LAYER_COMMIT + l));
     // field checks
-    VFieldProof F{};
+    VFieldProof& F = plan.fproof;
+    F = VFieldProof{};
     F.z = st.z;
     F.zg = st.zg;
     F.hz = st.hz;
@@ -554,13 +550,9 @@ bool plan_proof(const VState& st, size_t blob_off, VerifyPlan& plan, std::string
     F.rem_len = (uint32_t)(pf.fri_rem.n / (8 * de));
     F.nl = nl;
     F.de = (uint32_t)de;
-    F.logN = ilog2(N);
-    const uint32_t fi = (uint32_t)plan.fproofs.size();
-    plan.fproofs.push_back(F);
-    plan.fidx.push_back((int)fi);
+    F.logN = depthN;
     for (u64 i = 0; i < nu; i++) {
         VFieldQuery Q{};
-        Q.proof = fi;
         Q.pos = st.pos[i];
         Q.trace_off = off(pf.trace_rows.p + i * 56);
         Q.cons_off = off(pf.constraint_rows.p + i * 8 * de);
@@ -577,19 +569,12 @@ bool plan_proof(const VState& st, size_t blob_off, VerifyPlan& plan, std::string
     return true;
 }
 
-std::string finish_proof(const VState& st, const std::vector<Digest>& roots, uint32_t flags) {
+std::string finish_proof(const VState& st, uint32_t flags) {
     const ParsedProof& pf = st.pf;
-    // roots[t] for the 2 + nl trees (an all-ones digest marks a structurally invalid opening)
-    auto bad_root = [&](size_t t) {
-        const Digest& d = roots[t];
-        bool invalid = true;
-        for (int w = 0; w < 8; w++) invalid = invalid && d.w[w] == 0xFFFFFFFFu;
-        return invalid || !same(d, pf.com[t]);
-    };
-    if (bad_root(0)) return "TraceQueryDoesNotMatchCommitment";
-    if (bad_root(1)) return "ConstraintQueryDoesNotMatchCommitment";
+    if (flags & VF_TRACE) return "TraceQueryDoesNotMatchCommitment";
+    if (flags & VF_CONSTRAINT) return "ConstraintQueryDoesNotMatchCommitment";
     for (unsigned l = 0; l < st.nl; l++) {
-        if (bad_root(2 + l)) return "FriVerificationFailed(LayerCommitmentMismatch)";
+        if (flags & (1u << (VF_LAYER_COMMIT + l))) return "FriVerificationFailed(LayerCommitmentMismatch)";
         if (flags & (1u << l)) return "FriVerificationFailed(InvalidLayerFolding)";
     }
     const u64 rl = pf.fri_rem.n / (8 * st.de);
@@ -597,7 +582,7 @@ std::string finish_proof(const VState& st, const std::vector<Digest>& roots, uin
     memcpy(raw.data(), pf.fri_rem.p, rl * 8 * st.de);
     if (!same(hash_elements(raw.data(), rl * st.de), pf.com[2 + st.nl]))
         return "FriVerificationFailed(RemainderCommitmentMismatch)";
-    if (flags & (1u << 31)) return "FriVerificationFailed(InvalidRemainderFolding)";
+    if (flags & VF_REMAINDER) return "FriVerificationFailed(InvalidRemainderFolding)";
     return "";
 }
 

@@ -32,6 +32,7 @@ struct ParsedProof {
     Opts o{};
     u64 num_unique = 0;
     std::vector<Digest> com;  // trace root, constraint root, FRI layer roots, remainder commitment
+    const uint8_t* com_p = nullptr;  // the commitments' bytes in the proof
     Span trace_rows, constraint_rows, ood, hz, fri_rem;
     Paths trace_paths, constraint_paths;
     std::vector<Span> fri_vals;
@@ -77,18 +78,29 @@ AirConst air_of(const xfg_air_consts* a);
 
 namespace xfg {
 
-// ---- batched GPU verification: the host replays every transcript, then the Merkle openings
-// (leaf hashes + level-by-level merges over all proofs at once) and the per-query DEEP / FRI /
-// remainder checks run on the device.
+// ---- batched GPU verification: the host replays every transcript and lists, per proof, its 2 + nl
+// batch Merkle openings and its queries; the device then verifies every opening with one workgroup
+// (leaf hashes, BatchMerkleProof::get_root level by level, root comparison: vtree_kernel) and runs
+// the per-query DEEP / FRI / remainder checks (vfield_kernel).
 constexpr int VMAXL = 12;  // FRI layers
-struct VLeaf {
-    u64 src;          // byte offset in the proof blob
-    uint32_t words;   // u64 words hashed (1, 2, 7, 8 or 16)
-    uint32_t dst;     // digest slot
+// flags[proof] bits set by the device: 0..11 FRI layer l folding, 16..27 FRI layer l commitment,
+// 29 constraint commitment, 30 trace commitment, 31 remainder folding
+constexpr uint32_t VF_TRACE = 1u << 30, VF_CONSTRAINT = 1u << 29, VF_REMAINDER = 1u << 31;
+constexpr int VF_LAYER_COMMIT = 16;
+struct VTree {
+    u64 root_off;           // blob offset of the commitment the root must equal
+    uint32_t leaf0, nidx;   // opened leaves: tleaves[leaf0 .. leaf0 + nidx), sorted by index
+    uint32_t vec0, nvec;    // node vectors: vecs[vec0 .. vec0 + nvec), in the proof's order
+    uint32_t words, depth;  // u64 words per leaf (1, 2, 7, 8 or 16); log2 leaves
+    uint32_t proof, bit;    // on failure: flags[proof] |= bit
 };
-struct VGather {
-    u64 src;
-    uint32_t dst, pad;
+struct VTreeLeaf {
+    u64 index;    // leaf index
+    u64 row_off;  // blob offset of the opened row
+};
+struct VVec {
+    u64 off;  // blob offset of the vector's first digest
+    uint32_t cnt, pad;
 };
 struct VFieldProof {
     E2 z, zg, hz, gam, dc[7], ood[14];
@@ -101,27 +113,21 @@ struct VFieldQuery {
     u64 pos, trace_off, cons_off;
     u64 row_off[VMAXL];  // layer l: blob offset of the opened row of 8 E values
 };
+// one proof's part of a batch (blob offsets already global; tree / vector / proof indices local)
 struct VerifyPlan {
-    std::vector<uint8_t> blob;                 // all proofs back to back
-    std::vector<VGather> gathers;
-    std::vector<VLeaf> leaves;
-    std::vector<std::vector<uint32_t>> rounds; // per Merkle level: (out, left, right) slot triples
-    std::vector<VFieldProof> fproofs;
+    std::vector<VTree> trees;
+    std::vector<VTreeLeaf> tleaves;
+    std::vector<VVec> vecs;
+    VFieldProof fproof{};
     std::vector<VFieldQuery> fqueries;
-    uint32_t nslots = 0;
-    // per proof: root slots of its 2 + nl trees in check order (-1 = structurally invalid)
-    std::vector<std::vector<int64_t>> roots;
-    std::vector<int> fidx;                     // proof -> index into fproofs (-1: not planned)
 };
-// add one proof whose transcript replayed fine; false (+ err) on a structural error
+// plan one proof whose transcript replayed fine, its bytes at blob offset blob_off; false (+ err) on
+// a structural error the host verifier reports before any opening is checked
 bool plan_proof(const VState& st, size_t blob_off, VerifyPlan& plan, std::string& err);
-// empty a plan for reuse, keeping its allocations
-void reset_plan(VerifyPlan& plan);
 // the host part after the device work: first failing check in the verifier's order, "" if none
-std::string finish_proof(const VState& st, const std::vector<Digest>& roots, uint32_t flags);
+std::string finish_proof(const VState& st, uint32_t flags);
 
-void launch_verify(const uint8_t* blob, const VGather* g, u64 ng, const VLeaf* lv, u64 nleaf,
-                   const uint32_t* rounds, const u64* round_off, int nrounds, const VFieldProof* fp,
-                   const VFieldQuery* fq, u64 nq, Digest* dig, uint32_t* flags, hipStream_t s);
+void launch_verify(const uint8_t* blob, const VTree* trees, u64 ntrees, const VTreeLeaf* tleaves, const VVec* vecs,
+                   const VFieldProof* fp, const VFieldQuery* fq, u64 nq, uint32_t* flags, hipStream_t s);
 
 }  // namespace xfg

@@ -16,18 +16,6 @@ __device__ __forceinline__ u64 ld_u64(const uint8_t* p) {
 }
 __device__ __forceinline__ E2 ld_e(const uint8_t* p, int de) { return de == 2 ? E2{ld_u64(p), ld_u64(p + 8)} : E2{ld_u64(p), 0}; }
 
-__global__ void vgather_kernel(const uint8_t* blob, const VGather* g, u64 n, Digest* dig) {
-    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint8_t* p = blob + g[i].src;
-    Digest d;
-#pragma unroll
-    for (int w = 0; w < 8; w++)
-        d.w[w] = (uint32_t)p[4 * w] | ((uint32_t)p[4 * w + 1] << 8) | ((uint32_t)p[4 * w + 2] << 16) |
-                 ((uint32_t)p[4 * w + 3] << 24);
-    dig[g[i].dst] = d;
-}
-
 template <int K>
 __device__ __forceinline__ Digest hash_words(const uint8_t* p) {
     u64 v[K];
@@ -35,25 +23,145 @@ __device__ __forceinline__ Digest hash_words(const uint8_t* p) {
     for (int k = 0; k < K; k++) v[k] = ld_u64(p + 8 * k);
     return b3_hash_elems<K>(v);
 }
-__global__ void vleaf_kernel(const uint8_t* blob, const VLeaf* lv, u64 n, Digest* dig) {
-    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const VLeaf L = lv[i];
-    const uint8_t* p = blob + L.src;
-    Digest d;
-    switch (L.words) {  // trace row 7, constraint value 1 / 2, FRI row 8 / 16
-        case 1: d = hash_words<1>(p); break;
-        case 2: d = hash_words<2>(p); break;
-        case 7: d = hash_words<7>(p); break;
-        case 8: d = hash_words<8>(p); break;
-        default: d = hash_words<16>(p); break;
+__device__ Digest hash_row(const uint8_t* p, uint32_t words) {
+    switch (words) {  // trace row 7, constraint value 1 / 2, FRI row 8 / 16
+        case 1: return hash_words<1>(p);
+        case 2: return hash_words<2>(p);
+        case 7: return hash_words<7>(p);
+        case 8: return hash_words<8>(p);
+        default: return hash_words<16>(p);
     }
-    dig[L.dst] = d;
 }
-__global__ void vmerge_kernel(const uint32_t* t, u64 n, Digest* dig) {
-    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    dig[t[3 * i]] = b3_merge(dig[t[3 * i + 1]], dig[t[3 * i + 2]]);
+__device__ __forceinline__ Digest ld_digest(const uint8_t* p) {
+    Digest d;
+#pragma unroll
+    for (int w = 0; w < 8; w++)
+        d.w[w] = (uint32_t)p[4 * w] | ((uint32_t)p[4 * w + 1] << 8) | ((uint32_t)p[4 * w + 2] << 16) |
+                 ((uint32_t)p[4 * w + 3] << 24);
+    return d;
+}
+
+// exclusive prefix count of `f` over the workgroup's 256 threads (4 waves), and the total
+__device__ __forceinline__ int block_scan(bool f, int* wsum, int& total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long m = __ballot(f);
+    const int pre = __popcll(m & ((1ULL << lane) - 1));
+    if (lane == 0) wsum[w] = __popcll(m);
+    __syncthreads();
+    int base = 0;
+    total = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        base += k < w ? wsum[k] : 0;
+        total += wsum[k];
+    }
+    __syncthreads();
+    return base + pre;
+}
+
+// One batch Merkle opening per workgroup: BatchMerkleProof::get_root (winter-crypto 0.8.3, the
+// opening plan_batch_opening emits) recomputed in place. Thread i hashes opened row i (rows sorted
+// by leaf index); the distinct leaf pairs take their missing leaf from node vector j (j = the pair's
+// position); then, level by level, the entry at position j of the current sorted list merges with
+// its right neighbour when that is its sibling, else takes its sibling from vector j; the survivors
+// are compacted (block scan) and climb one level. The opening is valid when every vector holds
+// exactly the nodes the walk takes and the root equals the commitment; else flags[proof] |= bit.
+__global__ __launch_bounds__(256) void vtree_kernel(const uint8_t* blob, const VTree* trees, const VTreeLeaf* tleaves,
+                                                    const VVec* vecs, uint32_t* flags) {
+    __shared__ Digest leaf[512];
+    __shared__ Digest dg[2][256];
+    __shared__ u64 hx[2][256];
+    __shared__ u64 sidx[256];
+    __shared__ uint8_t have[512];
+    __shared__ int wsum[4];
+    __shared__ int bad;
+    const VTree T = trees[blockIdx.x];
+    const int i = threadIdx.x;
+    const u64 L = 1ULL << T.depth;
+    if (i == 0) bad = 0;
+    // the vector this thread's position consumes from, and how many nodes it has taken
+    VVec vec{0, 0, 0};
+    if (i < (int)T.nvec) vec = vecs[T.vec0 + i];
+    uint32_t used = 0;
+    auto take = [&](Digest& out) {
+        if (used >= vec.cnt) {
+            bad = 1;
+            out = Digest{};
+            return;
+        }
+        out = ld_digest(blob + vec.off + 32 * (u64)used);
+        used++;
+    };
+    u64 idx = 0;
+    Digest ld{};
+    const bool opened = i < (int)T.nidx;
+    if (opened) {
+        const VTreeLeaf lf = tleaves[T.leaf0 + i];
+        idx = lf.index;
+        ld = hash_row(blob + lf.row_off, T.words);
+        sidx[i] = idx;
+    }
+    have[i] = 0;
+    have[i + 256] = 0;
+    __syncthreads();
+    // leaf pairs: thread i's pair position = number of pair starts before it (minus one if it is the
+    // right leaf of a pair whose left leaf is opened too)
+    const bool start = opened && (i == 0 || (sidx[i - 1] >> 1) != (idx >> 1));
+    int npairs;
+    const int pp = block_scan(start, wsum, npairs) - (opened && !start ? 1 : 0);
+    if (opened) {
+        leaf[2 * pp + (idx & 1)] = ld;
+        have[2 * pp + (idx & 1)] = 1;
+        if (start) hx[0][pp] = (L + (idx & ~1ULL)) >> 1;
+    }
+    if (i == 0 && (int)T.nvec != npairs) bad = 1;
+    __syncthreads();
+    if (i < npairs) {
+        Digest l = leaf[2 * i], r = leaf[2 * i + 1];
+        if (!have[2 * i]) take(l);
+        if (!have[2 * i + 1]) take(r);
+        dg[0][i] = b3_merge(l, r);
+    }
+    __syncthreads();
+    int nn = npairs, cb = 0;
+    for (unsigned lvl = 1; lvl < T.depth; lvl++) {
+        const bool act = i < nn;
+        const u64 h = act ? hx[cb][i] : 0;
+        const bool left = act && !(h & 1) && i + 1 < nn && hx[cb][i + 1] == h + 1;
+        const bool right = act && (h & 1) && i > 0 && hx[cb][i - 1] == h - 1;
+        Digest par{};
+        if (act && !right) {  // one merge call site: (own, right neighbour) or (own, vector node) in order
+            Digest x = dg[cb][i], y;
+            if (left) {
+                y = dg[cb][i + 1];
+            } else {
+                take(y);
+                if (h & 1) {
+                    const Digest t = x;
+                    x = y;
+                    y = t;
+                }
+            }
+            par = b3_merge(x, y);
+        }
+        int total;
+        const int m = block_scan(act && !right, wsum, total);
+        if (act && !right) {
+            hx[cb ^ 1][m] = h >> 1;
+            dg[cb ^ 1][m] = par;
+        }
+        __syncthreads();
+        nn = total;
+        cb ^= 1;
+    }
+    if (i < (int)T.nvec && used != vec.cnt) bad = 1;
+    __syncthreads();
+    if (i == 0) {
+        const Digest root = ld_digest(blob + T.root_off);
+        bool ok = !bad && nn == 1 && hx[cb][0] == 1;
+        for (int w = 0; w < 8; w++) ok = ok && dg[cb][0].w[w] == root.w[w];
+        if (!ok) atomicOr(&flags[T.proof], T.bit);
+    }
 }
 
 // apply_drp of one row: iDFT_8 on the coset x<w_8> (per coordinate), evaluate at alpha
@@ -121,17 +229,9 @@ __global__ __launch_bounds__(64) void vfield_kernel(const uint8_t* blob, const V
 
 static unsigned blocks_for(u64 n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
-void launch_verify(const uint8_t* blob, const VGather* g, u64 ng, const VLeaf* lv, u64 nleaf,
-                   const uint32_t* rounds, const u64* round_off, int nrounds, const VFieldProof* fp,
-                   const VFieldQuery* fq, u64 nq, Digest* dig, uint32_t* flags, hipStream_t s) {
-    if (ng) hipLaunchKernelGGL(vgather_kernel, dim3(blocks_for(ng, 256)), dim3(256), 0, s, blob, g, ng, dig);
-    if (nleaf) hipLaunchKernelGGL(vleaf_kernel, dim3(blocks_for(nleaf, 256)), dim3(256), 0, s, blob, lv, nleaf, dig);
-    for (int r = 0; r < nrounds; r++) {
-        const u64 cnt = (round_off[r + 1] - round_off[r]) / 3;
-        if (cnt)
-            hipLaunchKernelGGL(vmerge_kernel, dim3(blocks_for(cnt, 256)), dim3(256), 0, s, rounds + round_off[r], cnt,
-                               dig);
-    }
+void launch_verify(const uint8_t* blob, const VTree* trees, u64 ntrees, const VTreeLeaf* tleaves, const VVec* vecs,
+                   const VFieldProof* fp, const VFieldQuery* fq, u64 nq, uint32_t* flags, hipStream_t s) {
+    if (ntrees) hipLaunchKernelGGL(vtree_kernel, dim3((unsigned)ntrees), dim3(256), 0, s, blob, trees, tleaves, vecs, flags);
     if (nq) hipLaunchKernelGGL(vfield_kernel, dim3(blocks_for(nq, 64)), dim3(64), 0, s, blob, fp, fq, nq, flags);
     (void)hipGetLastError();
 }
