@@ -90,6 +90,9 @@ void xfg_ctx_destroy(xfg_ctx* ctx);
 int xfg_default_options(xfg_options* out);
 /* length of the error text of the last failing call on ctx (copied NUL-terminated into buf) */
 int xfg_last_error(const xfg_ctx* ctx, char* buf, size_t len);
+/* the largest proof the prover emits for (trace_length, opts): a tight upper bound computed section
+ * by section (every proof fits; configs[2]: 98.8 KB for ~78 KB proofs), so callers can size fixed
+ * per-proof output slots, e.g. the exchange records of a sharded run; 0 for unsupported shapes */
 size_t xfg_proof_size_bound(uint64_t trace_length, const xfg_options* opts);
 
 /* prove_burn_mint; trace_length 0 -> 64 (the reference's fixed TraceInfo::new(7, 64)) */

@@ -462,8 +462,8 @@ struct ProofJob {
     int status = XFG_OK;
 };
 
-static void stage_mark(Lane* c, int k) {
-    if (c->timing) HIPCHK(hipEventRecord(c->ev[k], c->stream));
+static void stage_mark(Lane* c, int k, hipStream_t on = nullptr) {
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[k], on ? on : c->stream));
 }
 struct HostTrace {
     std::vector<std::pair<const char*, std::chrono::steady_clock::time_point>> m;
@@ -912,8 +912,9 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     // the gathers (a few hundred microseconds of small kernels) go to the lane's high-priority stream:
     // on its own stream a lane's gathers queued behind the other lanes' chains in the shared hardware
     // queue (XFG_TRACE: 3.1 ms mean, 9 ms p90 to sync them); the lane's stream s has drained
-    // (sync_rem), so they need no event
-    const hipStream_t sq = c->timing ? s : gather_stream(c);
+    // (sync_rem), so they need no event. Timing mode takes the same stream: stage 9 is measured from
+    // the lane stream's last event to an event behind the gathers' copies on this one
+    const hipStream_t sq = gather_stream(c);
     HIPCHK(hipMemcpyAsync(c->gidx.p, hidx, allidx.size() * 8, hipMemcpyHostToDevice, sq));
     ht.mark("q_h2d");
     {
@@ -954,7 +955,7 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     if (nvals) HIPCHK(hipMemcpyAsync(gv, c->gval.p, nvals * 8, hipMemcpyDeviceToHost, sq));
     if (ndig + 2 * nopen)
         HIPCHK(hipMemcpyAsync(gd, c->gdig.p, (ndig + 2 * nopen) * sizeof(Digest), hipMemcpyDeviceToHost, sq));
-    stage_mark(c, 9);
+    stage_mark(c, 9, sq);
     auto t_q1 = std::chrono::steady_clock::now();
     ht.mark("queries_host");
     HIPCHK(hipStreamSynchronize(sq));

@@ -39,10 +39,10 @@ struct Reader {
         return v;
     }
 };
-static bool read_paths(Reader& r, size_t len, Paths& out) {
-    const uint8_t* q = r.take(len);
-    if (!q) return false;
-    Reader s{q, len};
+// BatchMerkleProof node vectors inside a paths byte vector (u8 vector count, per vector u8 count +
+// digests): the content parse of VerifierChannel::new, after the options check
+static bool parse_paths(const Span& raw, Paths& out) {
+    Reader s{raw.p, raw.n};
     const u64 m = s.u(1);
     out.ptr.resize(m);
     out.cnt.resize(m);
@@ -53,7 +53,7 @@ static bool read_paths(Reader& r, size_t len, Paths& out) {
         out.ptr[i] = d;
         out.cnt[i] = (uint32_t)c;
     }
-    return !s.bad && s.off == len;
+    return !s.bad && s.off == raw.n;
 }
 static bool read_span(Reader& r, int len_bytes, Span& s) {
     s.n = r.u(len_bytes);
@@ -101,37 +101,45 @@ std::string parse_proof(const uint8_t* bytes, size_t len, ParsedProof& pf) {
     pf.com_p = c;
     if (clen) memcpy(pf.com.data(), c, clen);  // (an empty vector's data() may be null)
     if (r.u(1) != 1) return "ProofDeserializationError(\"trace queries: expected one segment\")";
-    if (!read_span(r, 4, pf.trace_rows)) return "ProofDeserializationError(\"trace queries\")";
-    const u64 tpl = r.u(4);
-    if (r.bad || !read_paths(r, tpl, pf.trace_paths)) return "ProofDeserializationError(\"trace query paths\")";
-    if (!read_span(r, 4, pf.constraint_rows)) return "ProofDeserializationError(\"constraint queries\")";
-    const u64 cpl = r.u(4);
-    if (r.bad || !read_paths(r, cpl, pf.constraint_paths))
-        return "ProofDeserializationError(\"constraint query paths\")";
-    Span hz;
-    if (!read_span(r, 2, pf.ood) || !read_span(r, 2, hz)) return "ProofDeserializationError(\"OOD frame\")";
-    const size_t esz = 8 * (size_t)pf.o.ext;  // bytes per E element
-    // frame of two rows (current, next) of `width` E values each: exactly that many, so every
-    // reader of the frame (verifier, xfg_proof_parse) stays inside the proof bytes
-    if (pf.ood.n != 1 + 2 * pf.width * esz || pf.ood.p[0] != 2 || hz.n != esz)
-        return "ProofDeserializationError(\"OOD frame layout\")";
-    pf.ood.p += 1;
-    pf.ood.n -= 1;
-    pf.hz = hz;
+    // StarkProof::read_from keeps every section below as a byte vector; their contents (Merkle node
+    // vectors, the OOD frame layout, the remainder's element size) are parsed by parse_contents
+    // after the acceptable-options check, as VerifierChannel::new does
+    if (!read_span(r, 4, pf.trace_rows) || !read_span(r, 4, pf.trace_paths_raw))
+        return "ProofDeserializationError(\"trace queries\")";
+    if (!read_span(r, 4, pf.constraint_rows) || !read_span(r, 4, pf.constraint_paths_raw))
+        return "ProofDeserializationError(\"constraint queries\")";
+    if (!read_span(r, 2, pf.ood_raw) || !read_span(r, 2, pf.hz)) return "ProofDeserializationError(\"OOD frame\")";
     const u64 nl = r.u(1);
     pf.fri_vals.resize(nl);
-    pf.fri_paths.resize(nl);
-    for (u64 l = 0; l < nl; l++) {
-        if (!read_span(r, 4, pf.fri_vals[l])) return "ProofDeserializationError(\"FRI layer values\")";
-        const u64 pl = r.u(4);
-        if (r.bad || !read_paths(r, pl, pf.fri_paths[l])) return "ProofDeserializationError(\"FRI layer paths\")";
-    }
-    if (!read_span(r, 2, pf.fri_rem) || pf.fri_rem.n % esz) return "ProofDeserializationError(\"FRI remainder\")";
+    pf.fri_paths_raw.resize(nl);
+    for (u64 l = 0; l < nl; l++)
+        if (!read_span(r, 4, pf.fri_vals[l]) || !read_span(r, 4, pf.fri_paths_raw[l]))
+            return "ProofDeserializationError(\"FRI layer\")";
+    if (!read_span(r, 2, pf.fri_rem)) return "ProofDeserializationError(\"FRI remainder\")";
     pf.partitions = r.u(1);
     pf.nonce = r.u(8);
     if (r.bad) return "ProofDeserializationError(\"unexpected end of input\")";
     if (r.off != len) return "ProofDeserializationError(\"trailing bytes\")";
     pf.size = r.off;
+    return "";
+}
+
+// VerifierChannel::new's content parse of the byte-vector sections: "" or the
+// ProofDeserializationError
+std::string parse_contents(ParsedProof& pf) {
+    const size_t esz = 8 * (size_t)pf.o.ext;  // bytes per E element
+    if (!parse_paths(pf.trace_paths_raw, pf.trace_paths)) return "ProofDeserializationError(\"trace query paths\")";
+    if (!parse_paths(pf.constraint_paths_raw, pf.constraint_paths))
+        return "ProofDeserializationError(\"constraint query paths\")";
+    // frame of two rows (current, next) of `width` E values each: exactly that many, so every
+    // reader of the frame stays inside the proof bytes
+    if (pf.ood_raw.n != 1 + 2 * pf.width * esz || pf.ood_raw.p[0] != 2 || pf.hz.n != esz)
+        return "ProofDeserializationError(\"OOD frame layout\")";
+    pf.ood = Span{pf.ood_raw.p + 1, pf.ood_raw.n - 1};
+    pf.fri_paths.resize(pf.fri_paths_raw.size());
+    for (size_t l = 0; l < pf.fri_paths_raw.size(); l++)
+        if (!parse_paths(pf.fri_paths_raw[l], pf.fri_paths[l])) return "ProofDeserializationError(\"FRI layer paths\")";
+    if (pf.fri_rem.n % esz) return "ProofDeserializationError(\"FRI remainder\")";
     return "";
 }
 
@@ -272,7 +280,9 @@ std::string verify_transcript(const uint8_t* bytes, size_t len, const AirConst& 
     if (memcmp(&o, &acceptable, sizeof o)) return "UnacceptableProofOptions";  // AcceptableOptions::OptionSet
     const u64 n = 1ULL << pf.logn;
     if (check_options(n, o)) return "UnacceptableProofOptions";
-    // VerifierChannel::new: the element sections are deserialised now
+    // VerifierChannel::new: the section contents and the element sections are deserialised now
+    e = parse_contents(pf);
+    if (!e.empty()) return e;
     bool canon = canonical_elems(pf.trace_rows) && canonical_elems(pf.constraint_rows) && canonical_elems(pf.ood) &&
                  canonical_elems(pf.hz) && canonical_elems(pf.fri_rem);
     for (const Span& v : pf.fri_vals) canon = canon && canonical_elems(v);
@@ -629,10 +639,13 @@ int xfg_proof_parse(const uint8_t* proof, size_t len, xfg_proof_info* info, char
     info->pow_nonce = pf.nonce;
     info->size = pf.size;
     for (size_t i = 0; i < 2 && i < pf.com.size(); i++) memcpy(i ? info->constraint_root : info->trace_root, pf.com[i].w, 32);
-    // with an extension: first coordinates; a frame narrower than 7 columns leaves the rest 0
-    const size_t frame = pf.ood.n / (8 * de);
-    for (size_t k = 0; k < 14 && k < frame; k++) info->ood_trace[k] = pf.ood.elem(k * de);
-    info->ood_composition = pf.hz.elem(0);
+    // with an extension: first coordinates; a frame narrower than 7 columns leaves the rest 0, and a
+    // frame whose contents do not parse (which from_bytes does not look at) leaves all of it 0
+    if (parse_contents(pf).empty()) {
+        const size_t frame = pf.ood.n / (8 * de);
+        for (size_t k = 0; k < 14 && k < frame; k++) info->ood_trace[k] = pf.ood.elem(k * de);
+        info->ood_composition = pf.hz.elem(0);
+    }
     return XFG_OK;
 }
 

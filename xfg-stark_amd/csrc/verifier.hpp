@@ -34,14 +34,18 @@ struct ParsedProof {
     std::vector<Digest> com;  // trace root, constraint root, FRI layer roots, remainder commitment
     const uint8_t* com_p = nullptr;  // the commitments' bytes in the proof
     Span trace_rows, constraint_rows, ood, hz, fri_rem;
+    Span trace_paths_raw, constraint_paths_raw, ood_raw;  // byte vectors as StarkProof::read_from keeps them
+    std::vector<Span> fri_vals, fri_paths_raw;
+    // filled by parse_contents
     Paths trace_paths, constraint_paths;
-    std::vector<Span> fri_vals;
     std::vector<Paths> fri_paths;
     u64 partitions = 0, nonce = 0;
     size_t size = 0;
 };
-// "" on success, else the ProofDeserializationError text
+// StarkProof::from_bytes, structural: "" on success, else the ProofDeserializationError text
 std::string parse_proof(const uint8_t* bytes, size_t len, ParsedProof& pf);
+// the sections' contents (VerifierChannel::new, after the options check)
+std::string parse_contents(ParsedProof& pf);
 
 // everything the query checks need, after the transcript has been replayed
 struct VState {
