@@ -79,16 +79,22 @@ class Exchange:
       gathered records D2H into a pinned ring slot, all on the side stream, with an event at the
       end; the host awaits it only when the slot comes round again or when the proofs are read.
 
+    With `threaded` the collectives and copies are issued -- and waited for -- by one worker thread
+    per rank, in the loop's order (so every rank issues the same sequence of collectives), and the
+    loop only hands work over and picks up completions.
+
     On the gloo backend (CPU rehearsal, tests/test_dist.py) the same steps run on host tensors and
     the collectives' Work handles stand in for the events."""
 
-    def __init__(self, rank, world, per, cap, device, dist, send_slots, recv_slots=3, lookahead=4):
+    def __init__(self, rank, world, per, cap, device, dist, send_slots, recv_slots=3, lookahead=4, threaded=False):
         import torch
         self.rank, self.world, self.per, self.cap = rank, world, per, cap
         self.device, self.dist, self.cuda = device, dist, device.type == "cuda"
         self.hdr = 8 * per
         self.rec = self.hdr + per * cap
-        self.stream = torch.cuda.Stream(device) if self.cuda else None
+        # XFG_EXCHANGE_PRIO=1: the side stream at the highest priority (bench A/B)
+        prio = -1 if os.environ.get("XFG_EXCHANGE_PRIO") == "1" else 0
+        self.stream = torch.cuda.Stream(device, priority=prio) if self.cuda else None
         self.send = [_pinned(self.rec, device) for _ in range(send_slots)]
         self.send_dev = [torch.empty(self.rec, dtype=torch.uint8, device=device)
                          for _ in range(send_slots)] if self.cuda else None
@@ -108,14 +114,49 @@ class Exchange:
             if self.cuda else None
         self.in_pending = [None] * ring
         self.packed, self.nsteps = None, 0
+        self.blocked = 0.0  # loop seconds spent waiting for earlier exchanges (XFG_BENCH_PHASES)
+        self.main_thread = threading_ident()
+        self.worker = None
+        if threaded:
+            import queue
+            import threading
+            self.jobs = queue.Queue()
+            self.worker = threading.Thread(target=self._work, daemon=True)
+            self.worker.start()
 
     def _done(self, h):
         if h is None:
             return
-        if self.cuda:
-            h.synchronize()  # torch.cuda.Event at the end of the side stream's work
+        t = time.perf_counter()
+        if isinstance(h, _Job) or not self.cuda:
+            h.wait()  # worker job, or the collective's Work (gloo)
         else:
-            h.wait()  # the collective's Work (gloo)
+            h.synchronize()  # torch.cuda.Event at the end of the side stream's work
+        if threading_ident() == self.main_thread:
+            self.blocked += time.perf_counter() - t
+
+    def _work(self):
+        import torch
+        if self.cuda:
+            torch.cuda.set_device(self.device)
+        while True:
+            job = self.jobs.get()
+            if job is None:
+                return
+            fn, done = job
+            try:
+                self._done(fn())  # issue, then wait for it here rather than in the loop
+            except BaseException as e:  # surfaced by the loop's wait on `done`
+                done.err = e
+            done.ev.set()
+
+    def _run(self, fn):
+        """fn issues an operation and returns its completion handle: run it now, or on the worker"""
+        if self.worker is None:
+            return fn()
+        job = _Job()
+        self.jobs.put((fn, job))
+        return job
 
     def _side(self):
         import contextlib
@@ -139,15 +180,16 @@ class Exchange:
     def _scatter(self, i):
         slot = i % len(self.in_pending)
         chunks = list(self.packed[i].unbind(0)) if self.rank == 0 else None
-        if self.cuda:
-            with self._side():
-                w = self.dist.scatter(self.in_dev[slot], chunks, src=0, async_op=True)
-                w.wait()  # the side stream waits for the collective; the host does not
-                self.in_host[slot].copy_(self.in_dev[slot], non_blocking=True)
-                h = self._event()
-        else:
-            h = self.dist.scatter(self.in_host[slot], chunks, src=0, async_op=True)
-        self.in_pending[slot] = (i, h)
+
+        def issue():
+            if self.cuda:
+                with self._side():
+                    w = self.dist.scatter(self.in_dev[slot], chunks, src=0, async_op=True)
+                    w.wait()  # the side stream waits for the collective; the host does not
+                    self.in_host[slot].copy_(self.in_dev[slot], non_blocking=True)
+                    return self._event()
+            return self.dist.scatter(self.in_host[slot], chunks, src=0, async_op=True)
+        self.in_pending[slot] = (i, self._run(issue))
 
     def inputs(self, i):
         """step i's shard as prove kwargs (issues step i + lookahead's scatter)"""
@@ -176,22 +218,25 @@ class Exchange:
     def gather(self, s):
         """record s holds a complete batch: send it to rank 0 (asynchronous); returns a Gathered"""
         r = None
-        with self._side():
-            if self.rank == 0:
-                r = self.next_recv
-                self.next_recv = (r + 1) % len(self.recv_busy)
+        if self.rank == 0:
+            r = self.next_recv
+            self.next_recv = (r + 1) % len(self.recv_busy)
+            if self.worker is None:  # (the worker runs its jobs in order: slot r's last gather is done)
                 self._done(self.recv_busy[r])
-            if self.cuda:
-                self.send_dev[s].copy_(self.send[s], non_blocking=True)
-                got = list(self.recv_dev[r].unbind(0)) if self.rank == 0 else None
-                w = self.dist.gather(self.send_dev[s], got, dst=0, async_op=True)
-                w.wait()
-                if self.rank == 0:
-                    self.recv_host[r].copy_(self.recv_dev[r], non_blocking=True)
-                h = self._event()
-            else:
+
+        def issue():
+            with self._side():
+                if self.cuda:
+                    self.send_dev[s].copy_(self.send[s], non_blocking=True)
+                    got = list(self.recv_dev[r].unbind(0)) if self.rank == 0 else None
+                    w = self.dist.gather(self.send_dev[s], got, dst=0, async_op=True)
+                    w.wait()
+                    if self.rank == 0:
+                        self.recv_host[r].copy_(self.recv_dev[r], non_blocking=True)
+                    return self._event()
                 got = list(self.recv_host[r].unbind(0)) if self.rank == 0 else None
-                h = self.dist.gather(self.send[s], got, dst=0, async_op=True)
+                return self.dist.gather(self.send[s], got, dst=0, async_op=True)
+        h = self._run(issue)
         self.send_busy[s] = h
         self.send_owned[s] = False
         if r is not None:
@@ -201,6 +246,25 @@ class Exchange:
     def drain(self):
         for h in self.send_busy + self.recv_busy:
             self._done(h)
+
+
+def threading_ident():
+    import threading
+    return threading.get_ident()
+
+
+class _Job:
+    """completion of an exchange operation issued and awaited by the worker thread"""
+
+    def __init__(self):
+        import threading
+        self.ev = threading.Event()
+        self.err = None
+
+    def wait(self):
+        self.ev.wait()
+        if self.err is not None:
+            raise self.err
 
 
 class Gathered:
@@ -265,6 +329,7 @@ def pipelined_steps(submit_fn, collect_fn, batches, depth=2, ex=None, packed=Non
 
     t0 = clk()
     if ex is not None:
+        ex.blocked = 0.0
         ex.start_inputs(packed, len(batches))
     for i, b in enumerate(batches):
         t1 = clk()
@@ -299,7 +364,9 @@ def pipelined_steps(submit_fn, collect_fn, batches, depth=2, ex=None, packed=Non
         print("submitted ms: " + " ".join(f"{t * 1e3:.1f}" for t in ts), file=sys.stderr)
     if ph is not None:
         print("phases ms: " + " ".join(f"{k}={v * 1e3:.1f}" for k, v in ph.items()) +
-              f" total={(clk() - t0) * 1e3:.1f}", file=sys.stderr)
+              f" total={(clk() - t0) * 1e3:.1f}" +
+              (f" (of which waiting on earlier exchanges {ex.blocked * 1e3:.1f})" if ex is not None else ""),
+              file=sys.stderr)
     return out
 
 
@@ -549,7 +616,10 @@ def main():
                   for b in batches]
         # the exchange's pinned records and device buffers (setup): one send record per batch in
         # flight plus the ones whose gathers may still run
-        ex = Exchange(rank, world, per, prover.proof_size_bound(n), device, dist, send_slots=args.depth + 3)
+        ex = Exchange(rank, world, per, prover.proof_size_bound(n), device, dist, send_slots=args.depth + 3,
+                      recv_slots=int(os.environ.get("XFG_EXCHANGE_SLOTS", "3")),
+                      lookahead=int(os.environ.get("XFG_EXCHANGE_AHEAD", "4")),
+                      threaded=os.environ.get("XFG_EXCHANGE_THREAD", "0") == "1")
 
     def submit_fn(kws, record=None):
         if record is not None:  # sharded: proofs written straight into the exchange record

@@ -10,7 +10,7 @@ SHAPE=${SHAPE:-c5}
 if [ "$SHAPE" = c5 ]; then ARGS="1 20 16 5"; else ARGS="64 16 8 5"; fi
 PROG="import sys; sys.path.insert(0, 'xfg-stark_amd'); import xfgstark
 a = [int(x) for x in '$ARGS'.split()]
-p = xfgstark.XfgBurnMintProver(); p.prepare(a[0], 1 << a[1])
+p = xfgstark.XfgBurnMintProver()
 print('lde_ms', round(p.bench_lde(a[0], 1 << a[1], a[2], a[3]), 4))"
 for rep in $(seq 1 ${REPS:-2}); do
   for lv in $LIBS; do

@@ -44,7 +44,7 @@ class _FakeRecordBatch:
             C.memmove(self.addr + 8 * k + i * FAKE_CAP, p, len(p))
 
 
-def _worker(rank, world, port, per, ret, steps=3, depth=2, lookahead=4, fail=None):
+def _worker(rank, world, port, per, ret, steps=3, depth=2, lookahead=4, fail=None, threaded=False):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     for p in (os.path.join(root, "xfg-stark_amd"), root):
@@ -67,7 +67,7 @@ def _worker(rank, world, port, per, ret, steps=3, depth=2, lookahead=4, fail=Non
         return _FakeRecordBatch(kws, record, fail if rank == world - 1 else None)
 
     ex = bench.Exchange(rank, world, per, FAKE_CAP, torch.device("cpu"), dist, send_slots=depth + 3,
-                        lookahead=lookahead)
+                        lookahead=lookahead, threaded=threaded)
     try:
         out = bench.pipelined_steps(submit, None, batches, depth, ex, packed)
     except RuntimeError as e:
@@ -105,16 +105,18 @@ def _run(world, per, **kw):
     return out
 
 
-@pytest.mark.parametrize("world,per,steps,depth,lookahead", [
-    (2, 3, 1, 1, 4),   # one synchronous step
-    (2, 1, 3, 2, 1),   # scatter only one step ahead
-    (2, 2, 3, 2, 4),   # lookahead past the window
-    (2, 2, 5, 3, 2),
-    (4, 2, 4, 2, 3),   # four ranks
+@pytest.mark.parametrize("world,per,steps,depth,lookahead,threaded", [
+    (2, 3, 1, 1, 4, False),   # one synchronous step
+    (2, 1, 3, 2, 1, False),   # scatter only one step ahead
+    (2, 2, 3, 2, 4, False),   # lookahead past the window
+    (2, 2, 5, 3, 2, False),
+    (4, 2, 4, 2, 3, False),   # four ranks
+    (2, 2, 5, 3, 2, True),    # collectives issued by the exchange worker thread
+    (4, 1, 6, 2, 3, True),
 ])
-def test_exchange_gloo(world, per, steps, depth, lookahead):
+def test_exchange_gloo(world, per, steps, depth, lookahead, threaded):
     import synthetic
-    kind, out = _run(world, per, steps=steps, depth=depth, lookahead=lookahead)
+    kind, out = _run(world, per, steps=steps, depth=depth, lookahead=lookahead, threaded=threaded)
     assert kind == "ok"
     base = 100 * (steps - 1)  # the last step's inputs, in rank order
     want = _fake_prove([synthetic.burn_inputs(base + i) for i in range(per * world)])

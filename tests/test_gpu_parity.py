@@ -68,6 +68,18 @@ def test_lde_kernel_tile_paths_match_oracle(prover, n, blowup):
     assert np.array_equal(got, O.evaluate_lde_np(coef[0], blowup, 7))
 
 
+@pytest.mark.parametrize("blowup", [8, 16])
+def test_lde_r1024_kernels_two_polys_match_oracle(prover, blowup):
+    """ntt_pass_a_r1024 / ntt_pass_b_r1024 (n = 2^20 past the four-step tables): two polynomials, so
+    the (poly, coset) block numbering of the coset-consecutive order is exercised across polys"""
+    n = 1 << 20
+    rng = np.random.default_rng(blowup + 31)
+    coef = rng.integers(0, P, size=(2, n), dtype=np.uint64)
+    got = np.asarray(prover.debug_lde(coef, n, blowup))
+    for k in range(2):
+        assert np.array_equal(got[k], O.evaluate_lde_np(coef[k], blowup, 7)), k
+
+
 @pytest.mark.parametrize("n,off7", [(1 << 18, True), (1 << 22, False)])
 def test_interpolate_kernel_tile_paths_match_oracle(prover, n, off7):
     rng = np.random.default_rng(n + 11)

@@ -49,6 +49,31 @@ __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, u32 voff, u32 s
     __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)voff, (int)soff, 0);
 }
 
+// 16-byte stores of column pairs. A pass's last step leaves each lane the outputs of one column (pass
+// A) or row (pass B) at rows / positions base + r * stride, and lanes 2i, 2i + 1 hold the two
+// neighbouring words of every such output line. One dword pair swapped between them (DPP quad_perm
+// [1, 0, 3, 2], folded into the selects) lets the even lane store both words of the even outputs and
+// the odd lane both words of the odd ones: half as many store instructions, 16 B per lane. (A wave
+// ending a tile with 32 8-byte stores per lane is store-issue-bound: MI355X_MICROARCH.md, "store
+// tail".) Full tiles only: both lanes of a pair must hold a group.
+typedef u64 u64x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u64 swap_lane_pair(u64 x) {
+    const int lo = __builtin_amdgcn_mov_dpp((int)(u32)x, 0xB1, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(u32)(x >> 32), 0xB1, 0xF, 0xF, false);
+    return (u64)(u32)lo | ((u64)(u32)hi << 32);
+}
+// at(r): address of output r of the pair's EVEN word (16-byte aligned)
+template <int RR, class AT>
+__device__ __forceinline__ void store_pairs(const u64* v, AT at) {
+    const bool odd = threadIdx.x & 1;
+#pragma unroll
+    for (int r = 0; r < RR; r += 2) {
+        const u64 g0 = swap_lane_pair(v[r]), g1 = swap_lane_pair(v[r + 1]);
+        const u64x2 d = {odd ? g1 : v[r], odd ? v[r + 1] : g0};
+        *reinterpret_cast<u64x2*>(at(odd ? r + 1 : r)) = d;
+    }
+}
+
 // LDS tile: row `seq` of length S at seq * PITCH; element i at i + (i >> P), one pad word per 2^P
 // elements, P = log2 elements per thread (4 or 5). The pad word makes the stride-2^P stores of a
 // full-radix first step (lanes along a row, 2^P contiguous outputs each) conflict-free: 16 lanes
@@ -372,6 +397,16 @@ __global__ __launch_bounds__(1 << LOGT, (1 << (10 - LOGT)) >> (LOGE - 4)) void n
         }
         u64 w = INV ? wq[q] : gl_mul(p7q[q], wq[q]);
         const u64 step = sq[q];
+        if (!INV && a.preg) {  // configs[4]-class forward pass: full tiles of 8 columns
+            u64 o[RR];
+#pragma unroll
+            for (int r = 0; r < RR; r++) {
+                o[r] = gl_mul(v[r], w);
+                if (r + 1 < RR) w = gl_mul(w, step);
+            }
+            store_pairs<RR>(o, [&](int r) { return y + ((u64)(base + r * stride) << a.logC) + (j2 & ~1ULL); });
+            return;
+        }
 #pragma unroll
         for (int r = 0; r < RR; r++) {
             y[((u64)(base + r * stride) << a.logC) + j2] = gl_mul(v[r], w);
@@ -507,6 +542,91 @@ __global__ __launch_bounds__(256, 4) void ntt_pass_a_cos2(NttArgs a) {
         }
     }
 }
+
+// ---------------------------------------------------------------- pass A, R = 1024, no four-step table
+// Forward pass A of the LDEs past the four-step tables (configs[4]: 2^20 x 16, R = C = 1024, radix
+// 32 x 32): one (8-column tile, poly, coset) per 256-thread block, a tile's cosets side by side on one
+// XCD (xcd_block_coset: the coefficient tile comes from HBM once, from L2 beta - 1 times). The coset
+// pre-factor g_t^j1 (g_t = 7^C w_(beta R)^t), j1 = j0 + 32 r, splits into an element factor g_t^(32 r)
+// -- the same for every lane, read from the pass table by scalar loads -- and a group factor g_t^j0
+// that rides on the second step's twiddle: a per-coset [r][k] table w_1024^(r k) g_t^r in LDS. No
+// per-lane pre-factor loads, so the first step's loads hold 64 VGPRs, not 128. The exchange between
+// the two radix-32 steps goes through the LDS tile in 32-bit halves (pass_dft_split: 42 KiB per
+// block, three blocks per CU); the four-step twiddles are running products applied at the store,
+// which writes column pairs (store_pairs).
+__global__ __launch_bounds__(256, 3) void ntt_pass_a_r1024(NttArgs a) {
+    constexpr int LOGR = 10, LOGE = 5, NT = 256, R = 1 << LOGR, RR = 32, logTC = 3, TC = 1 << logTC;
+    constexpr int PITCH = row_pitch(R, LOGE, NT_LOG2(NT) + LOGE - LOGR);
+    extern __shared__ u64 lds[];
+    u32* tile = reinterpret_cast<u32*>(lds);
+    u64* comb = lds + (TC * PITCH + 1) / 2;
+    int bx, by;
+    xcd_block_coset(a.logbeta, bx, by);
+    const int pt = by, col0 = bx * TC, poly = pt >> a.logbeta, t = pt & ((1 << a.logbeta) - 1);
+    const u64 n = 1ULL << a.logn;
+    const int logN = a.logn + a.logbeta;
+    const u64 maskN = (1ULL << logN) - 1;
+    const u64* pre = a.pt + R + (1 << a.logC) + (u64)t * R;                                     // g_t^j1
+    const u64* comb_t = a.pt + R + (1 << a.logC) + ((u64)R << a.logbeta) + ((u64)t << LOGR);  // [r][k]
+    for (int i = threadIdx.x; i < R; i += NT) comb[i] = comb_t[i];
+    // (read only by the second step, behind pass_dft_split's first barrier)
+    const auto rin = buf_rsrc(a.in + (u64)poly * a.in_stride + col0);
+    auto ldg = [&](int seq, int j, int o) -> u64 {
+        return gl_mul(buf_ld(rin, (((u32)j << a.logC) + seq) * 8, ((u32)o << a.logC) * 8), pre[o]);
+    };
+    u64 p7 = 0, w0 = 0, stp = 0;
+    auto pf = [&](int, int seq, int base, int stride) {
+        const u64 j2 = col0 + seq;
+        p7 = a.T.pow7[j2];  // 7^j2 w_N^(j2 (t + beta base)); step w_n^(j2 stride)
+        w0 = tw_get(a.T, logN, (j2 * ((u64)t + ((u64)base << a.logbeta))) & maskN, false);
+        stp = tw_get(a.T, a.logn, (j2 * (u64)stride) & (n - 1), false);
+    };
+    u64* y = a.y + (u64)pt * n;
+    auto stg = [&](int, int seq, int base, int stride, u64* v) {
+        u64 w = gl_mul(p7, w0);
+#pragma unroll
+        for (int r = 0; r < RR; r++) {
+            v[r] = gl_mul(v[r], w);
+            if (r + 1 < RR) w = gl_mul(w, stp);
+        }
+        const u64 c2 = (u64)(col0 + seq) & ~1ULL;
+        store_pairs<RR>(v, [&](int r) { return y + ((u64)(base + r * stride) << a.logC) + c2; });
+    };
+    pass_dft_split<LOGR, LOGE, false, true, NT, decltype(ldg), decltype(stg), decltype(pf), true>(tile, logTC, comb,
+                                                                                                ldg, stg, pf);
+}
+size_t pass_a_r1024_lds() { return (size_t)((8 * row_pitch(1024, 5, 3) + 1) / 2 + 1024) * sizeof(u64); }
+
+// Forward pass B of the same LDEs: row DFTs of C = 1024 (radix 32 x 32), one 8-row tile per 256-thread
+// block with the exchange in 32-bit halves (three blocks per CU), canonical outputs stored as row
+// pairs (store_pairs) into the coset-major LDE
+__global__ __launch_bounds__(256, 3) void ntt_pass_b_r1024(NttArgs a) {
+    constexpr int LOGC = 10, LOGE = 5, NT = 256, C = 1 << LOGC, R1 = 32, G1 = C / R1, RR = 32, logTR = 3;
+    constexpr int TR = 1 << logTR, PITCH = row_pitch(C, LOGE, logTR);
+    extern __shared__ u64 lds[];
+    u32* tile = reinterpret_cast<u32*>(lds);
+    u64* ltw = lds + (TR * PITCH + 1) / 2;
+    int bx, by;
+    xcd_block(true, bx, by);
+    const int pt = by, k10 = bx * TR;
+    const u64 n = 1ULL << a.logn;
+    for (int i = threadIdx.x; i < C; i += NT) ltw[i] = a.pt[(1 << a.logR) + i];
+    const int seq0 = threadIdx.x / G1, j0 = threadIdx.x % G1;
+    const u64* y = a.y + (u64)pt * n + ((u64)(k10 + seq0) << LOGC) + j0;
+    u64 yv[R1];
+#pragma unroll
+    for (int r = 0; r < R1; r++) yv[r] = y[r * G1];
+    __syncthreads();
+    auto ldg = [&](int, int, int o) -> u64 { return yv[o / G1]; };
+    u64* out = a.out + (u64)pt * n + k10;
+    auto stg = [&](int, int seq, int base, int stride, u64* v) {
+#pragma unroll
+        for (int r = 0; r < RR; r++) v[r] = canon(v[r]);
+        store_pairs<RR>(v, [&](int r) { return out + (seq & ~1) + ((u64)(base + r * stride) << a.logR); });
+    };
+    pass_dft_split<LOGC, LOGE, false, false, NT>(tile, logTR, ltw, ldg, stg, NoPf{});
+}
+size_t pass_b_r1024_lds() { return (size_t)((8 * row_pitch(1024, 5, 3) + 1) / 2 + 1024) * sizeof(u64); }
 
 // ---------------------------------------------------------------- pass B: row DFTs (size C)
 template <int LOGC, bool INV, int LOGT, int LOGE>
@@ -669,11 +789,12 @@ __global__ __launch_bounds__(1 << LOGT, MINW) void ntt_pass_b_pers(NttArgs a, in
         u64 nx[R1];
         if (ti + per_x < tend) load(ti + per_x, nx);
         auto ldg = [&](int, int, int o) -> u64 { return yv[o / G1]; };
-        const auto rout = buf_rsrc(a.out + (u64)pt * n + k10);
+        u64* out = a.out + (u64)pt * n + k10;
         auto stg = [&](int, int seq, int base, int stride, u64* v) {
+            u64 o[RR];
 #pragma unroll
-            for (int r = 0; r < RR; r++)
-                buf_st(rout, (seq + ((u32)base << a.logR)) * 8, ((u32)(r * stride) << a.logR) * 8, canon(v[r]));
+            for (int r = 0; r < RR; r++) o[r] = canon(v[r]);
+            store_pairs<RR>(o, [&](int r) { return out + (seq & ~1) + ((u64)(base + r * stride) << a.logR); });
         };
         pass_dft<LOGC, LOGE, false, false, NT>(tile, logTR, ltw, ldg, stg, [](int, int, int, int) {});
 #pragma unroll
@@ -830,6 +951,12 @@ __global__ void pass_tables_kernel(u64* out, int logn, int logbeta, int logR, in
     } else if (!inv && i < R + C + (R << logbeta)) {
         const u64 t = (i - R - C) >> logR, j = (i - R - C) & (R - 1);
         out[i] = gl_mul(T.pow7[j << logC], tw_get(T, logR + logbeta, (t * j) & ((1ULL << (logR + logbeta)) - 1), false));
+    } else if (!inv && logR == 10 && i < R + C + 2 * (R << logbeta)) {
+        // ntt_pass_a_r1024: [t][r][k] = w_1024^(r k) g_t^r, g_t^r = 7^(C r) w_(beta R)^(t r)  (r, k < 32)
+        const u64 q = i - R - C - (R << logbeta);
+        const u64 t = q >> 10, r = (q >> 5) & 31, k = q & 31;
+        const u64 g = gl_mul(T.pow7[r << logC], tw_get(T, logR + logbeta, (t * r) & ((1ULL << (logR + logbeta)) - 1), false));
+        out[i] = gl_mul(tw_get(T, logR, r * k, false), g);
     } else if (!inv && logR == 8 && logbeta >= 2) {
         // ntt_pass_a_cos2: [t][r][k] = w_R^(r k) 7^(C r) w_(beta R)^(t r), then [c][r] = 7^(16 C r) w_(16 beta)^(c r)
         const u64 q = i - R - C - (R << logbeta);
@@ -844,8 +971,10 @@ __global__ void pass_tables_kernel(u64* out, int logn, int logbeta, int logR, in
         }
     }
 }
-// entries of the ntt_pass_a_cos2 tables appended to the forward pass tables (R = 256, beta >= 4)
+// entries of the ntt_pass_a_cos2 tables appended to the forward pass tables (R = 256, beta >= 4), or of
+// the ntt_pass_a_r1024 tables (R = 1024)
 static u64 cos2_extra(int logR, int logbeta) {
+    if (logbeta >= 0 && logR == 10) return 1ULL << (logR + logbeta);
     return (logbeta >= 0 && logR == 8 && logbeta >= 2) ? ((1ULL << (logR + logbeta)) + (16ULL << (logbeta - 2))) : 0;
 }
 u64 pass_tables_size(int logn, int logbeta) {
@@ -877,6 +1006,8 @@ void build_fourstep(u64* out, int logn, int logbeta, const Tables& T, hipStream_
                        logbeta, logR, logC, T);
 }
 
+constexpr bool kR1024 = true;
+constexpr bool kChunk = false;
 static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
     ntt_split(a.logn, a.logR, a.logC);
     const int R = 1 << a.logR, C = 1 << a.logC;
@@ -910,6 +1041,13 @@ static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
     if (inv) {
         run_pass_a<true>(a.logR, ltA, eA, ga, lds_a, s, a);
         run_pass_b<true>(a.logC, ltB, eB, gb, lds_b, s, a);
+        return;
+    }
+    if (kR1024 && !a.t4 && a.pt && a.logR == 10 && a.logC == 10 && eA == 5 && eB == 5) {
+        // past the four-step tables at n = 2^20 (configs[4])
+        const size_t la = pass_a_r1024_lds(), lb = pass_b_r1024_lds();
+        hipLaunchKernelGGL(ntt_pass_a_r1024, dim3(C >> 3, npoly << a.logbeta), dim3(256), la, s, a);
+        hipLaunchKernelGGL(ntt_pass_b_r1024, dim3(R >> 3, npoly << a.logbeta), dim3(256), lb, s, a);
         return;
     }
     // pass A: all cosets of a column tile in one block where the four-step table exists (R = 256):
@@ -958,7 +1096,19 @@ void launch_lde(const u64* coef, u64 coef_stride, u64* out, u64* scratch, int np
     a.t4 = (T.fs && logn <= FOURSTEP_MAX_LOG && logbeta <= 4) ? T.fs->fwd[logn][logbeta] : nullptr;
     a.pt = a.t4 ? a.t4 + fourstep_main(logn, logbeta)
                 : ((T.fs && logn <= PASS_MAX_LOG && logbeta <= 4) ? T.fs->pass_fwd[logn][logbeta] : nullptr);
-    ntt_run(a, npoly, false, s);
+    if (a.t4 || !kChunk) {
+        ntt_run(a, npoly, false, s);
+        return;
+    }
+    // past the four-step tables: one polynomial per launch pair, so its intermediate (beta n words,
+    // 128 MiB at 2^20 x 16) is read back by pass B from the 256 MiB Infinity Cache
+    const u64 N = 1ULL << (logn + logbeta);
+    for (int p = 0; p < npoly; p++) {
+        NttArgs b = a;
+        b.in = coef + (u64)p * coef_stride;
+        b.out = out + (u64)p * N;
+        ntt_run(b, 1, false, s);
+    }
 }
 
 void launch_interpolate(const u64* evals, u64 in_stride, u64* out, u64 out_stride, u64* scratch, int npoly, int logn,
