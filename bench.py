@@ -67,107 +67,119 @@ def _pinned(nbytes, device):
 class Exchange:
     """The exchange step of a sharded run (BASELINE configs[3]: 512 proofs over 8 GPUs; the reference's
     batch pattern is src/burn_mint_verifier.rs:326-338): rank 0 scatters each step's packed inputs,
-    every rank proves its shard, rank 0 gathers the proofs. Nothing here makes the host wait on the
-    GPU inside a step:
+    every rank proves its shard, rank 0 gathers the proofs.
 
-    * inputs -- one scatter per step, issued `lookahead` steps before the step is submitted
-      (asynchronous collective on a side stream, a non-blocking D2H of the shard into pinned memory,
-      an event); the submission syncs that event, long complete by then;
+    * inputs -- one scatter per step, issued `lookahead` steps before the step is submitted, then a
+      D2H of the shard into a pinned ring slot; the submission waits for that job, long done by then;
     * proofs -- every rank's batch is proven straight into a fixed-size pinned record (int64 lengths,
       then one xfg_proof_size_bound slot per proof: no packing copy, no size all-reduce). Once the
-      batch is done the record goes H2D into an asynchronous gather to rank 0, which copies the
-      gathered records D2H into a pinned ring slot, all on the side stream, with an event at the
-      end; the host awaits it only when the slot comes round again or when the proofs are read.
+      batch is done the record goes H2D, is gathered to rank 0 and copied D2H into a pinned ring slot
+      there.
 
-    With `threaded` the collectives and copies are issued -- and waited for -- by one worker thread
-    per rank, in the loop's order (so every rank issues the same sequence of collectives), and the
-    loop only hands work over and picks up completions.
+    Both run on worker threads (one for scatters, one for gathers, each with its own process group
+    and high-priority side stream, so each issues its collectives in step order on every rank) that
+    sequence the steps on the HOST: a copy or collective is issued only once what it reads is
+    complete, so no stream ever waits on another. A cross-stream wait is a barrier packet in one of
+    the few hardware queues the prover's lane streams share, and it holds every lane kernel queued
+    behind it until the other stream's work is done (round 4: with the collectives chained on the
+    GPU the exchange cost 9-15 % of the proving throughput at world size 1). The proving loop only
+    hands work over and, at the end, picks up the last gather.
 
     On the gloo backend (CPU rehearsal, tests/test_dist.py) the same steps run on host tensors and
-    the collectives' Work handles stand in for the events."""
+    the collectives' Work handles are waited for directly."""
 
-    def __init__(self, rank, world, per, cap, device, dist, send_slots, recv_slots=3, lookahead=4, threaded=False):
+    def __init__(self, rank, world, per, cap, device, dist, send_slots, recv_slots=4, lookahead=4):
+        import queue
+        import threading
         import torch
         self.rank, self.world, self.per, self.cap = rank, world, per, cap
         self.device, self.dist, self.cuda = device, dist, device.type == "cuda"
         self.hdr = 8 * per
         self.rec = self.hdr + per * cap
-        # XFG_EXCHANGE_PRIO=1: the side stream at the highest priority (bench A/B)
-        prio = -1 if os.environ.get("XFG_EXCHANGE_PRIO") == "1" else 0
-        self.stream = torch.cuda.Stream(device, priority=prio) if self.cuda else None
+        opts = None
+        if self.cuda and hasattr(dist, "ProcessGroupNCCL"):
+            opts = dist.ProcessGroupNCCL.Options()
+            opts.is_high_priority_stream = True  # RCCL's own streams off the lanes' hardware queues
+        mk = getattr(dist, "new_group", None)
+        self.g_in = mk(pg_options=opts) if mk else None
+        self.g_out = mk(pg_options=opts) if mk else None
+        for g in (self.g_in, self.g_out):  # communicators set up here, in the same order on every rank
+            if g is not None:
+                dist.barrier(group=g)
+        self.s_in = torch.cuda.Stream(device, priority=-1) if self.cuda else None
+        self.s_out = torch.cuda.Stream(device, priority=-1) if self.cuda else None
         self.send = [_pinned(self.rec, device) for _ in range(send_slots)]
-        self.send_dev = [torch.empty(self.rec, dtype=torch.uint8, device=device)
-                         for _ in range(send_slots)] if self.cuda else None
-        self.send_busy = [None] * send_slots  # completion handle of the gather that last read the slot
+        self.send_busy = [None] * send_slots  # the gather job that last read the slot
         self.send_owned = [False] * send_slots  # claimed by a batch that has not been gathered yet
         self.next_send = 0
-        self.recv_busy = [None] * recv_slots
-        self.next_recv = 0
+        # one device record each way: the gather worker runs one gather at a time
+        self.send_dev = torch.empty(self.rec, dtype=torch.uint8, device=device) if self.cuda else None
+        self.next_recv, self.recv_slots = 0, recv_slots
         if rank == 0:
             self.recv_host = [_pinned(world * self.rec, device).view(world, self.rec) for _ in range(recv_slots)]
-            self.recv_dev = [torch.empty((world, self.rec), dtype=torch.uint8, device=device)
-                             for _ in range(recv_slots)] if self.cuda else None
+            self.recv_dev = torch.empty((world, self.rec), dtype=torch.uint8, device=device) if self.cuda else None
         self.lookahead = max(1, lookahead)
         ring = self.lookahead + 1
         self.in_host = [_pinned(per * REC, device).view(per, REC) for _ in range(ring)]
-        self.in_dev = [torch.empty((per, REC), dtype=torch.uint8, device=device) for _ in range(ring)] \
-            if self.cuda else None
+        self.in_dev = torch.empty((per, REC), dtype=torch.uint8, device=device) if self.cuda else None
         self.in_pending = [None] * ring
         self.packed, self.nsteps = None, 0
-        self.blocked = 0.0  # loop seconds spent waiting for earlier exchanges (XFG_BENCH_PHASES)
-        self.main_thread = threading_ident()
-        self.worker = None
-        if threaded:
-            import queue
-            import threading
-            self.jobs = queue.Queue()
-            self.worker = threading.Thread(target=self._work, daemon=True)
-            self.worker.start()
+        self.blocked = 0.0  # loop seconds spent waiting for exchange jobs (XFG_BENCH_PHASES)
+        self.q_in, self.q_out = queue.Queue(), queue.Queue()
+        self.workers = [threading.Thread(target=self._work, args=(q,), daemon=True) for q in (self.q_in, self.q_out)]
+        for t in self.workers:
+            t.start()
 
-    def _done(self, h):
-        if h is None:
-            return
-        t = time.perf_counter()
-        if isinstance(h, _Job) or not self.cuda:
-            h.wait()  # worker job, or the collective's Work (gloo)
-        else:
-            h.synchronize()  # torch.cuda.Event at the end of the side stream's work
-        if threading_ident() == self.main_thread:
-            self.blocked += time.perf_counter() - t
-
-    def _work(self):
+    def _work(self, q):
         import torch
         if self.cuda:
             torch.cuda.set_device(self.device)
         while True:
-            job = self.jobs.get()
+            job = q.get()
             if job is None:
                 return
             fn, done = job
             try:
-                self._done(fn())  # issue, then wait for it here rather than in the loop
+                fn()
             except BaseException as e:  # surfaced by the loop's wait on `done`
                 done.err = e
             done.ev.set()
 
-    def _run(self, fn):
-        """fn issues an operation and returns its completion handle: run it now, or on the worker"""
-        if self.worker is None:
-            return fn()
+    def _submit(self, q, fn):
         job = _Job()
-        self.jobs.put((fn, job))
+        q.put((fn, job))
         return job
 
-    def _side(self):
-        import contextlib
-        import torch
-        return torch.cuda.stream(self.stream) if self.cuda else contextlib.nullcontext()
+    def _done(self, job):
+        if job is None:
+            return
+        t = time.perf_counter()
+        job.wait()
+        self.blocked += time.perf_counter() - t
 
-    def _event(self):
+    def _coll(self, stream, op, *args, **kw):
+        """issue a collective from `stream` and wait for it on the host only (Work.wait() would
+        make the stream wait on RCCL's stream on the GPU)"""
         import torch
-        ev = torch.cuda.Event()
-        ev.record(self.stream)
-        return ev
+        if not self.cuda:
+            op(*args, async_op=True, **kw).wait()
+            return
+        with torch.cuda.stream(stream):
+            w = op(*args, async_op=True, **kw)
+        while not w.is_completed():
+            time.sleep(2e-5)
+
+    def _copy(self, stream, dst, src):
+        import torch
+        with torch.cuda.stream(stream):
+            dst.copy_(src, non_blocking=True)
+        stream.synchronize()
+
+    def close(self):
+        for q in (self.q_in, self.q_out):
+            q.put(None)
+        for t in self.workers:
+            t.join()
 
     # ---- inputs
     def start_inputs(self, packed, nsteps):
@@ -181,15 +193,12 @@ class Exchange:
         slot = i % len(self.in_pending)
         chunks = list(self.packed[i].unbind(0)) if self.rank == 0 else None
 
-        def issue():
+        def job():
+            dst = self.in_dev if self.cuda else self.in_host[slot]
+            self._coll(self.s_in, self.dist.scatter, dst, chunks, src=0, group=self.g_in)
             if self.cuda:
-                with self._side():
-                    w = self.dist.scatter(self.in_dev[slot], chunks, src=0, async_op=True)
-                    w.wait()  # the side stream waits for the collective; the host does not
-                    self.in_host[slot].copy_(self.in_dev[slot], non_blocking=True)
-                    return self._event()
-            return self.dist.scatter(self.in_host[slot], chunks, src=0, async_op=True)
-        self.in_pending[slot] = (i, self._run(issue))
+                self._copy(self.s_in, self.in_host[slot], self.in_dev)
+        self.in_pending[slot] = (i, self._submit(self.q_in, job))
 
     def inputs(self, i):
         """step i's shard as prove kwargs (issues step i + lookahead's scatter)"""
@@ -216,45 +225,35 @@ class Exchange:
         return s, self.send[s].data_ptr(), self.rec
 
     def gather(self, s):
-        """record s holds a complete batch: send it to rank 0 (asynchronous); returns a Gathered"""
+        """record s holds a complete batch: send it to rank 0 (asynchronous); returns a Gathered,
+        whose proofs stay valid until recv_slots later gathers reuse its ring slot"""
         r = None
         if self.rank == 0:
             r = self.next_recv
-            self.next_recv = (r + 1) % len(self.recv_busy)
-            if self.worker is None:  # (the worker runs its jobs in order: slot r's last gather is done)
-                self._done(self.recv_busy[r])
+            self.next_recv = (r + 1) % self.recv_slots
 
-        def issue():
-            with self._side():
-                if self.cuda:
-                    self.send_dev[s].copy_(self.send[s], non_blocking=True)
-                    got = list(self.recv_dev[r].unbind(0)) if self.rank == 0 else None
-                    w = self.dist.gather(self.send_dev[s], got, dst=0, async_op=True)
-                    w.wait()
-                    if self.rank == 0:
-                        self.recv_host[r].copy_(self.recv_dev[r], non_blocking=True)
-                    return self._event()
+        def job():
+            if self.cuda:
+                self._copy(self.s_out, self.send_dev, self.send[s])
+                got = list(self.recv_dev.unbind(0)) if self.rank == 0 else None
+                self._coll(self.s_out, self.dist.gather, self.send_dev, got, dst=0, group=self.g_out)
+                if self.rank == 0:
+                    self._copy(self.s_out, self.recv_host[r], self.recv_dev)
+            else:
                 got = list(self.recv_host[r].unbind(0)) if self.rank == 0 else None
-                return self.dist.gather(self.send[s], got, dst=0, async_op=True)
-        h = self._run(issue)
+                self._coll(None, self.dist.gather, self.send[s], got, dst=0, group=self.g_out)
+        h = self._submit(self.q_out, job)
         self.send_busy[s] = h
         self.send_owned[s] = False
-        if r is not None:
-            self.recv_busy[r] = h
         return Gathered(self, h, r)
 
     def drain(self):
-        for h in self.send_busy + self.recv_busy:
+        for h in self.send_busy + [p[1] for p in self.in_pending if p]:
             self._done(h)
 
 
-def threading_ident():
-    import threading
-    return threading.get_ident()
-
-
 class _Job:
-    """completion of an exchange operation issued and awaited by the worker thread"""
+    """completion of an exchange job run by a worker thread"""
 
     def __init__(self):
         import threading
@@ -616,10 +615,7 @@ def main():
                   for b in batches]
         # the exchange's pinned records and device buffers (setup): one send record per batch in
         # flight plus the ones whose gathers may still run
-        ex = Exchange(rank, world, per, prover.proof_size_bound(n), device, dist, send_slots=args.depth + 3,
-                      recv_slots=int(os.environ.get("XFG_EXCHANGE_SLOTS", "3")),
-                      lookahead=int(os.environ.get("XFG_EXCHANGE_AHEAD", "4")),
-                      threaded=os.environ.get("XFG_EXCHANGE_THREAD", "0") == "1")
+        ex = Exchange(rank, world, per, prover.proof_size_bound(n), device, dist, send_slots=args.depth + 3)
 
     def submit_fn(kws, record=None):
         if record is not None:  # sharded: proofs written straight into the exchange record
@@ -670,6 +666,8 @@ def main():
             want = [p.to_bytes() for p in prover.prove_batch(batches[-1], trace_length=n)]
             assert last == want, "gathered proofs differ from a direct prove_batch"
 
+    if ex is not None:
+        ex.close()
     if rank != 0:  # the side measurements below are rank 0's
         prover.close()
         dist.barrier()
@@ -720,6 +718,8 @@ def main():
         "exchange": None if ex is None else {
             "backend": backend, "scatter": f"one per step, issued {ex.lookahead} steps ahead",
             "gather": "one per step: fixed record of 8 B lengths + proof-size-bound slots per rank",
+            "sequencing": "host worker threads (one per direction, own process group, high-priority "
+                          "streams); no cross-stream waits on the GPU",
             "record_bytes_per_rank": ex.rec, "proof_size_bound": ex.cap},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,

@@ -10,9 +10,10 @@ for rep in 1 2; do
     echo -n "$kv: "
     env ${kv//,/ } timeout -k 10 180 python3 -c "
 import sys; sys.path.insert(0, 'xfg-stark_amd'); sys.path.insert(0, '.')
+import torch; torch.cuda.init()
 import xfgstark, bench
 p = xfgstark.XfgBurnMintProver()
-c5 = bench.config5(p)
+c5 = bench.config5(p, 0)
 print('c5 proofs/s', c5['proofs_per_s'], 'trace lde ms', c5['trace_lde_ms'])" || exit 1
   done
 done

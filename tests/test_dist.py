@@ -44,7 +44,7 @@ class _FakeRecordBatch:
             C.memmove(self.addr + 8 * k + i * FAKE_CAP, p, len(p))
 
 
-def _worker(rank, world, port, per, ret, steps=3, depth=2, lookahead=4, fail=None, threaded=False):
+def _worker(rank, world, port, per, ret, steps=3, depth=2, lookahead=4, fail=None):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     for p in (os.path.join(root, "xfg-stark_amd"), root):
@@ -67,7 +67,7 @@ def _worker(rank, world, port, per, ret, steps=3, depth=2, lookahead=4, fail=Non
         return _FakeRecordBatch(kws, record, fail if rank == world - 1 else None)
 
     ex = bench.Exchange(rank, world, per, FAKE_CAP, torch.device("cpu"), dist, send_slots=depth + 3,
-                        lookahead=lookahead, threaded=threaded)
+                        lookahead=lookahead)
     try:
         out = bench.pipelined_steps(submit, None, batches, depth, ex, packed)
     except RuntimeError as e:
@@ -79,6 +79,7 @@ def _worker(rank, world, port, per, ret, steps=3, depth=2, lookahead=4, fail=Non
             ret.put(("ok", [bytes(x) for x in out]))  # rank 0 holds zero-copy views into the ring
     else:
         assert out is None
+    ex.close()
     dist.barrier()
     dist.destroy_process_group()
 
@@ -105,18 +106,17 @@ def _run(world, per, **kw):
     return out
 
 
-@pytest.mark.parametrize("world,per,steps,depth,lookahead,threaded", [
-    (2, 3, 1, 1, 4, False),   # one synchronous step
-    (2, 1, 3, 2, 1, False),   # scatter only one step ahead
-    (2, 2, 3, 2, 4, False),   # lookahead past the window
-    (2, 2, 5, 3, 2, False),
-    (4, 2, 4, 2, 3, False),   # four ranks
-    (2, 2, 5, 3, 2, True),    # collectives issued by the exchange worker thread
-    (4, 1, 6, 2, 3, True),
+@pytest.mark.parametrize("world,per,steps,depth,lookahead", [
+    (2, 3, 1, 1, 4),   # one synchronous step
+    (2, 1, 3, 2, 1),   # scatter only one step ahead
+    (2, 2, 3, 2, 4),   # lookahead past the window
+    (2, 2, 5, 3, 2),
+    (4, 2, 4, 2, 3),   # four ranks
+    (4, 1, 9, 2, 3),   # more steps than send records and receive slots
 ])
-def test_exchange_gloo(world, per, steps, depth, lookahead, threaded):
+def test_exchange_gloo(world, per, steps, depth, lookahead):
     import synthetic
-    kind, out = _run(world, per, steps=steps, depth=depth, lookahead=lookahead, threaded=threaded)
+    kind, out = _run(world, per, steps=steps, depth=depth, lookahead=lookahead)
     assert kind == "ok"
     base = 100 * (steps - 1)  # the last step's inputs, in rank order
     want = _fake_prove([synthetic.burn_inputs(base + i) for i in range(per * world)])
@@ -140,6 +140,9 @@ class _Work:
     def wait(self):
         pass
 
+    def is_completed(self):
+        return True
+
 
 class _LoopbackDist:
     """two "ranks" in one process, seen from rank 0: rank 1's record is handed to rank 0's gather
@@ -149,11 +152,11 @@ class _LoopbackDist:
     def __init__(self, other):
         self.other = other
 
-    def scatter(self, t, chunks, src=0, async_op=False):
+    def scatter(self, t, chunks, src=0, group=None, async_op=False):
         t.copy_(chunks[0])
         return _Work()
 
-    def gather(self, t, got, dst=0, async_op=False):
+    def gather(self, t, got, dst=0, group=None, async_op=False):
         got[0].copy_(t)
         got[1].copy_(self.other.to(t.device))
         return _Work()
@@ -240,6 +243,7 @@ def test_exchange_device_branch():
         out = ex.gather(s).proofs()
         assert [bytes(x) for x in out] == mine + theirs
     ex.drain()
+    ex.close()
 
 
 @pytest.mark.gpu
