@@ -7,7 +7,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 SHAPE=${SHAPE:-c5}
-if [ "$SHAPE" = c5 ]; then ARGS="1 20 16 5"; else ARGS="64 16 8 5"; fi
+if [ "$SHAPE" = c5 ]; then ARGS=${ARGS:-"1 20 16 5"}; else ARGS=${ARGS:-"64 16 8 5"}; fi
 PROG="import sys; sys.path.insert(0, 'xfg-stark_amd'); import xfgstark
 a = [int(x) for x in '$ARGS'.split()]
 p = xfgstark.XfgBurnMintProver()

@@ -564,8 +564,6 @@ __global__ __launch_bounds__(256, 3) void ntt_pass_a_r1024(NttArgs a) {
     xcd_block_coset(a.logbeta, bx, by);
     const int pt = by, col0 = bx * TC, poly = pt >> a.logbeta, t = pt & ((1 << a.logbeta) - 1);
     const u64 n = 1ULL << a.logn;
-    const int logN = a.logn + a.logbeta;
-    const u64 maskN = (1ULL << logN) - 1;
     const u64* pre = a.pt + R + (1 << a.logC) + (u64)t * R;                                     // g_t^j1
     const u64* comb_t = a.pt + R + (1 << a.logC) + ((u64)R << a.logbeta) + ((u64)t << LOGR);  // [r][k]
     for (int i = threadIdx.x; i < R; i += NT) comb[i] = comb_t[i];
@@ -574,12 +572,20 @@ __global__ __launch_bounds__(256, 3) void ntt_pass_a_r1024(NttArgs a) {
     auto ldg = [&](int seq, int j, int o) -> u64 {
         return gl_mul(buf_ld(rin, (((u32)j << a.logC) + seq) * 8, ((u32)o << a.logC) * 8), pre[o]);
     };
+    // four-step twiddle of output k1 = base + 32 q of column j2 (base < 32: the last step's group):
+    // 7^j2 w_N^(j2 (t + beta k1)) = [7^j2 w_N^(j2 t)] [w_n^(j2 base)] w_n^(32 j2 q), the two seed factors and
+    // the step read from small L2-resident tables (pass_tables_kernel; a gather from the 2^24-entry master
+    // table fetched a 128 B line for every 8 B it used)
+    const u64* xt = a.pt + R + (1 << a.logC) + ((u64)(2 * R) << a.logbeta);
+    const u64* seed_t = xt + ((u64)t << 10);
+    const u64* seed_b = xt + ((u64)1 << (10 + a.logbeta));
+    const u64* step_t = seed_b + (32 << 10);
     u64 p7 = 0, w0 = 0, stp = 0;
-    auto pf = [&](int, int seq, int base, int stride) {
-        const u64 j2 = col0 + seq;
-        p7 = a.T.pow7[j2];  // 7^j2 w_N^(j2 (t + beta base)); step w_n^(j2 stride)
-        w0 = tw_get(a.T, logN, (j2 * ((u64)t + ((u64)base << a.logbeta))) & maskN, false);
-        stp = tw_get(a.T, a.logn, (j2 * (u64)stride) & (n - 1), false);
+    auto pf = [&](int, int seq, int base, int) {
+        const int j2 = col0 + seq;
+        p7 = seed_t[j2];
+        w0 = seed_b[(base << 10) + j2];
+        stp = step_t[j2];
     };
     u64* y = a.y + (u64)pt * n;
     auto stg = [&](int, int seq, int base, int stride, u64* v) {
@@ -957,6 +963,21 @@ __global__ void pass_tables_kernel(u64* out, int logn, int logbeta, int logR, in
         const u64 t = q >> 10, r = (q >> 5) & 31, k = q & 31;
         const u64 g = gl_mul(T.pow7[r << logC], tw_get(T, logR + logbeta, (t * r) & ((1ULL << (logR + logbeta)) - 1), false));
         out[i] = gl_mul(tw_get(T, logR, r * k, false), g);
+    } else if (!inv && logR == 10 && i < R + C + 2 * (R << logbeta) + (C << logbeta) + 33 * C) {
+        // ntt_pass_a_r1024's four-step running-product seeds and step, from small tables instead of
+        // gathers from the master table: [t][j2] 7^j2 w_N^(j2 t), [b][j2] w_n^(j2 b) (b < 32), [j2] w_n^(32 j2)
+        const u64 q = i - R - C - 2 * (R << logbeta);
+        const int logn = logR + logC, logN = logn + logbeta;
+        if (q < (C << logbeta)) {
+            const u64 t = q >> logC, j2 = q & (C - 1);
+            out[i] = gl_mul(T.pow7[j2], tw_get(T, logN, (j2 * t) & ((1ULL << logN) - 1), false));
+        } else if (q < (C << logbeta) + 32 * C) {
+            const u64 b = (q - (C << logbeta)) >> logC, j2 = q & (C - 1);
+            out[i] = tw_get(T, logn, (j2 * b) & ((1ULL << logn) - 1), false);
+        } else {
+            const u64 j2 = q & (C - 1);
+            out[i] = tw_get(T, logn, (32 * j2) & ((1ULL << logn) - 1), false);
+        }
     } else if (!inv && logR == 8 && logbeta >= 2) {
         // ntt_pass_a_cos2: [t][r][k] = w_R^(r k) 7^(C r) w_(beta R)^(t r), then [c][r] = 7^(16 C r) w_(16 beta)^(c r)
         const u64 q = i - R - C - (R << logbeta);
@@ -973,14 +994,14 @@ __global__ void pass_tables_kernel(u64* out, int logn, int logbeta, int logR, in
 }
 // entries of the ntt_pass_a_cos2 tables appended to the forward pass tables (R = 256, beta >= 4), or of
 // the ntt_pass_a_r1024 tables (R = 1024)
-static u64 cos2_extra(int logR, int logbeta) {
-    if (logbeta >= 0 && logR == 10) return 1ULL << (logR + logbeta);
+static u64 cos2_extra(int logR, int logC, int logbeta) {
+    if (logbeta >= 0 && logR == 10) return (1ULL << (logR + logbeta)) + (1ULL << (logC + logbeta)) + (33ULL << logC);
     return (logbeta >= 0 && logR == 8 && logbeta >= 2) ? ((1ULL << (logR + logbeta)) + (16ULL << (logbeta - 2))) : 0;
 }
 u64 pass_tables_size(int logn, int logbeta) {
     int logR, logC;
     ntt_split(logn, logR, logC);
-    return (1ULL << logR) + (1ULL << logC) + (logbeta >= 0 ? (1ULL << (logR + logbeta)) : 0) + cos2_extra(logR, logbeta);
+    return (1ULL << logR) + (1ULL << logC) + (logbeta >= 0 ? (1ULL << (logR + logbeta)) : 0) + cos2_extra(logR, logC, logbeta);
 }
 void build_pass_tables(u64* out, int logn, int logbeta, const Tables& T, hipStream_t s) {
     int logR, logC;
@@ -994,7 +1015,7 @@ u64 fourstep_size(int logn, int logbeta) {
     int logR, logC;
     ntt_split(logn, logR, logC);
     return fourstep_main(logn, logbeta) + (1ULL << logR) + (1ULL << logC) + (logbeta >= 0 ? (1ULL << (logR + logbeta)) : 0) +
-           cos2_extra(logR, logbeta);
+           cos2_extra(logR, logC, logbeta);
 }
 void build_fourstep(u64* out, int logn, int logbeta, const Tables& T, hipStream_t s) {
     int logR, logC;
