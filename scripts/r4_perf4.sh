@@ -1,6 +1,7 @@
 #!/bin/bash
 # round 4: exchange-step variants at world size 1 (bench.py --dist under torch.distributed.run) against
-# the plain loop, interleaved; then a kernel trace of one --dist run (RCCL kernels and copies vs prover)
+# the plain loop, interleaved; then a kernel trace of one --dist run (RCCL kernels and copies vs prover).
+# Ran against the round-3 exchange of commit 4965fcf, whose XFG_EXCHANGE_* knobs are gone since d190dfe.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
