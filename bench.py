@@ -77,14 +77,17 @@ class Exchange:
       batch is done the record goes H2D, is gathered to rank 0 and copied D2H into a pinned ring slot
       there.
 
-    Both run on worker threads (one for scatters, one for gathers, each with its own process group
-    and high-priority side stream, so each issues its collectives in step order on every rank) that
-    sequence the steps on the HOST: a copy or collective is issued only once what it reads is
+    Both run on one worker thread with its own process group and high-priority side stream, which
+    sequences the steps on the HOST: a copy or collective is issued only once what it reads is
     complete, so no stream ever waits on another. A cross-stream wait is a barrier packet in one of
     the few hardware queues the prover's lane streams share, and it holds every lane kernel queued
     behind it until the other stream's work is done (round 4: with the collectives chained on the
-    GPU the exchange cost 9-15 % of the proving throughput at world size 1). The proving loop only
-    hands work over and, at the end, picks up the last gather.
+    GPU the exchange cost 9-15 % of the proving throughput at world size 1). One worker, one group:
+    the loop hands it scatters and gathers in step order, the same on every rank, so every rank
+    issues the same sequence of collectives (two communicators driven from two threads could issue
+    them in different orders on different ranks, and RCCL kernels waiting for peers behind each
+    other in a hardware queue can deadlock). The proving loop only hands work over and, at the end,
+    picks up the last gather.
 
     On the gloo backend (CPU rehearsal, tests/test_dist.py) the same steps run on host tensors and
     the collectives' Work handles are waited for directly."""
@@ -102,13 +105,10 @@ class Exchange:
             opts = dist.ProcessGroupNCCL.Options()
             opts.is_high_priority_stream = True  # RCCL's own streams off the lanes' hardware queues
         mk = getattr(dist, "new_group", None)
-        self.g_in = mk(pg_options=opts) if mk else None
-        self.g_out = mk(pg_options=opts) if mk else None
-        for g in (self.g_in, self.g_out):  # communicators set up here, in the same order on every rank
-            if g is not None:
-                dist.barrier(group=g)
-        self.s_in = torch.cuda.Stream(device, priority=-1) if self.cuda else None
-        self.s_out = torch.cuda.Stream(device, priority=-1) if self.cuda else None
+        self.group = mk(pg_options=opts) if mk else None
+        if self.group is not None:
+            dist.barrier(group=self.group)  # the communicator is set up here, not in the timed steps
+        self.side = torch.cuda.Stream(device, priority=-1) if self.cuda else None
         self.send = [_pinned(self.rec, device) for _ in range(send_slots)]
         self.send_busy = [None] * send_slots  # the gather job that last read the slot
         self.send_owned = [False] * send_slots  # claimed by a batch that has not been gathered yet
@@ -126,10 +126,9 @@ class Exchange:
         self.in_pending = [None] * ring
         self.packed, self.nsteps = None, 0
         self.blocked = 0.0  # loop seconds spent waiting for exchange jobs (XFG_BENCH_PHASES)
-        self.q_in, self.q_out = queue.Queue(), queue.Queue()
-        self.workers = [threading.Thread(target=self._work, args=(q,), daemon=True) for q in (self.q_in, self.q_out)]
-        for t in self.workers:
-            t.start()
+        self.jobs = queue.Queue()
+        self.worker = threading.Thread(target=self._work, args=(self.jobs,), daemon=True)
+        self.worker.start()
 
     def _work(self, q):
         import torch
@@ -146,9 +145,9 @@ class Exchange:
                 done.err = e
             done.ev.set()
 
-    def _submit(self, q, fn):
+    def _submit(self, fn):
         job = _Job()
-        q.put((fn, job))
+        self.jobs.put((fn, job))
         return job
 
     def _done(self, job):
@@ -177,10 +176,8 @@ class Exchange:
         stream.synchronize()
 
     def close(self):
-        for q in (self.q_in, self.q_out):
-            q.put(None)
-        for t in self.workers:
-            t.join()
+        self.jobs.put(None)
+        self.worker.join()
 
     # ---- inputs
     def start_inputs(self, packed, nsteps):
@@ -196,10 +193,10 @@ class Exchange:
 
         def job():
             dst = self.in_dev if self.cuda else self.in_host[slot]
-            self._coll(self.s_in, self.dist.scatter, dst, chunks, src=0, group=self.g_in)
+            self._coll(self.side, self.dist.scatter, dst, chunks, src=0, group=self.group)
             if self.cuda:
-                self._copy(self.s_in, self.in_host[slot], self.in_dev)
-        self.in_pending[slot] = (i, self._submit(self.q_in, job))
+                self._copy(self.side, self.in_host[slot], self.in_dev)
+        self.in_pending[slot] = (i, self._submit(job))
 
     def inputs(self, i):
         """step i's shard as prove kwargs (issues step i + lookahead's scatter)"""
@@ -235,15 +232,15 @@ class Exchange:
 
         def job():
             if self.cuda:
-                self._copy(self.s_out, self.send_dev, self.send[s])
+                self._copy(self.side, self.send_dev, self.send[s])
                 got = list(self.recv_dev.unbind(0)) if self.rank == 0 else None
-                self._coll(self.s_out, self.dist.gather, self.send_dev, got, dst=0, group=self.g_out)
+                self._coll(self.side, self.dist.gather, self.send_dev, got, dst=0, group=self.group)
                 if self.rank == 0:
-                    self._copy(self.s_out, self.recv_host[r], self.recv_dev)
+                    self._copy(self.side, self.recv_host[r], self.recv_dev)
             else:
                 got = list(self.recv_host[r].unbind(0)) if self.rank == 0 else None
-                self._coll(None, self.dist.gather, self.send[s], got, dst=0, group=self.g_out)
-        h = self._submit(self.q_out, job)
+                self._coll(None, self.dist.gather, self.send[s], got, dst=0, group=self.group)
+        h = self._submit(job)
         self.send_busy[s] = h
         self.send_owned[s] = False
         return Gathered(self, h, r)
@@ -721,8 +718,8 @@ def main():
         "exchange": None if ex is None else {
             "backend": backend, "scatter": f"one per step, issued {ex.lookahead} steps ahead",
             "gather": "one per step: fixed record of 8 B lengths + proof-size-bound slots per rank",
-            "sequencing": "host worker threads (one per direction, own process group, high-priority "
-                          "streams); no cross-stream waits on the GPU",
+            "sequencing": "one host worker thread (own process group, high-priority streams), "
+                          "collectives in step order; no cross-stream waits on the GPU",
             "record_bytes_per_rank": ex.rec, "proof_size_bound": ex.cap},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
