@@ -86,6 +86,15 @@ __device__ __forceinline__ void store_pairs(const u64* v, AT at) {
 __host__ __device__ constexpr int row_pitch(int S, int P = 4, int L = 4) {
     return P == 4 ? S + S / 16 + 1 : S + (S >> P) + ((L >= 4 || L <= 0) ? 1 : (16 >> L));
 }
+// Pitch of a 32-bit exchange tile (pass_dft_split). Its writes and ds_read_b32 / ds_read2_b32 reads
+// bank on (a / 4) mod 32 per 32-lane half, where a row-fast half-wave spans 2^L rows of the tile and
+// 32 / 2^L consecutive groups, so a row pitch of 32 / 2^L (mod 32) spreads the rows over distinct bank
+// groups. Radix 32 (P = 5): S + S / 32 + 32 / 2^L (the 64-bit pitch, 2 mod 32 at 8 rows, was 2-way
+// conflicted on pass A's first-step writes and both passes' second-step reads: 22 M conflict cycles
+// per configs[4] trace LDE). Radix 16 keeps row_pitch.
+__host__ __device__ constexpr int split_pitch(int S, int P, int L) {
+    return P == 5 ? S + (S >> 5) + ((32 >> L) & 31) : row_pitch(S, P, L);
+}
 template <int P>
 __device__ __forceinline__ int phys(int i) { return i + (i >> P); }
 // phys(j + o) for an offset o that is a compile-time constant after unrolling: a multiple of 2^P
@@ -224,7 +233,7 @@ __device__ __forceinline__ void pass_dft_split(u32* tile, int lognseq, const u64
     using PL = Plan<LOGS, LOGE>;
     static_assert(PL::NSTEP == 2 && PL::FIRST_LOGR == LOGE, "two full-radix steps");
     constexpr int L = NT_LOG2(NT) + LOGE - LOGS;
-    constexpr int PITCH = row_pitch(1 << LOGS, LOGE, L), E = 1 << LOGE, G = (1 << LOGS) / E;
+    constexpr int PITCH = split_pitch(1 << LOGS, LOGE, L), E = 1 << LOGE, G = (1 << LOGS) / E;
     auto nopf = [](int, int, int, int) {};
     u32 hi[E];
     int sseq = 0, sbase = 0;
@@ -556,7 +565,7 @@ __global__ __launch_bounds__(256, 4) void ntt_pass_a_cos2(NttArgs a) {
 // which writes column pairs (store_pairs).
 __global__ __launch_bounds__(256, 3) void ntt_pass_a_r1024(NttArgs a) {
     constexpr int LOGR = 10, LOGE = 5, NT = 256, R = 1 << LOGR, RR = 32, logTC = 3, TC = 1 << logTC;
-    constexpr int PITCH = row_pitch(R, LOGE, NT_LOG2(NT) + LOGE - LOGR);
+    constexpr int PITCH = split_pitch(R, LOGE, NT_LOG2(NT) + LOGE - LOGR);
     extern __shared__ u64 lds[];
     u32* tile = reinterpret_cast<u32*>(lds);
     u64* comb = lds + (TC * PITCH + 1) / 2;
@@ -601,14 +610,14 @@ __global__ __launch_bounds__(256, 3) void ntt_pass_a_r1024(NttArgs a) {
     pass_dft_split<LOGR, LOGE, false, true, NT, decltype(ldg), decltype(stg), decltype(pf), true>(tile, logTC, comb,
                                                                                                 ldg, stg, pf);
 }
-size_t pass_a_r1024_lds() { return (size_t)((8 * row_pitch(1024, 5, 3) + 1) / 2 + 1024) * sizeof(u64); }
+size_t pass_a_r1024_lds() { return (size_t)((8 * split_pitch(1024, 5, 3) + 1) / 2 + 1024) * sizeof(u64); }
 
 // Forward pass B of the same LDEs: row DFTs of C = 1024 (radix 32 x 32), one 8-row tile per 256-thread
 // block with the exchange in 32-bit halves (three blocks per CU), canonical outputs stored as row
 // pairs (store_pairs) into the coset-major LDE
 __global__ __launch_bounds__(256, 3) void ntt_pass_b_r1024(NttArgs a) {
     constexpr int LOGC = 10, LOGE = 5, NT = 256, C = 1 << LOGC, R1 = 32, G1 = C / R1, RR = 32, logTR = 3;
-    constexpr int TR = 1 << logTR, PITCH = row_pitch(C, LOGE, logTR);
+    constexpr int TR = 1 << logTR, PITCH = split_pitch(C, LOGE, logTR);
     extern __shared__ u64 lds[];
     u32* tile = reinterpret_cast<u32*>(lds);
     u64* ltw = lds + (TR * PITCH + 1) / 2;
@@ -632,7 +641,7 @@ __global__ __launch_bounds__(256, 3) void ntt_pass_b_r1024(NttArgs a) {
     };
     pass_dft_split<LOGC, LOGE, false, false, NT>(tile, logTR, ltw, ldg, stg, NoPf{});
 }
-size_t pass_b_r1024_lds() { return (size_t)((8 * row_pitch(1024, 5, 3) + 1) / 2 + 1024) * sizeof(u64); }
+size_t pass_b_r1024_lds() { return (size_t)((8 * split_pitch(1024, 5, 3) + 1) / 2 + 1024) * sizeof(u64); }
 
 // ---------------------------------------------------------------- pass B: row DFTs (size C)
 template <int LOGC, bool INV, int LOGT, int LOGE>
