@@ -1036,8 +1036,6 @@ void build_fourstep(u64* out, int logn, int logbeta, const Tables& T, hipStream_
                        logbeta, logR, logC, T);
 }
 
-constexpr bool kR1024 = true;
-constexpr bool kChunk = false;
 static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
     ntt_split(a.logn, a.logR, a.logC);
     const int R = 1 << a.logR, C = 1 << a.logC;
@@ -1073,7 +1071,7 @@ static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
         run_pass_b<true>(a.logC, ltB, eB, gb, lds_b, s, a);
         return;
     }
-    if (kR1024 && !a.t4 && a.pt && a.logR == 10 && a.logC == 10 && eA == 5 && eB == 5) {
+    if (!a.t4 && a.pt && a.logR == 10 && a.logC == 10 && eA == 5 && eB == 5) {
         // past the four-step tables at n = 2^20 (configs[4])
         const size_t la = pass_a_r1024_lds(), lb = pass_b_r1024_lds();
         hipLaunchKernelGGL(ntt_pass_a_r1024, dim3(C >> 3, npoly << a.logbeta), dim3(256), la, s, a);
@@ -1126,19 +1124,7 @@ void launch_lde(const u64* coef, u64 coef_stride, u64* out, u64* scratch, int np
     a.t4 = (T.fs && logn <= FOURSTEP_MAX_LOG && logbeta <= 4) ? T.fs->fwd[logn][logbeta] : nullptr;
     a.pt = a.t4 ? a.t4 + fourstep_main(logn, logbeta)
                 : ((T.fs && logn <= PASS_MAX_LOG && logbeta <= 4) ? T.fs->pass_fwd[logn][logbeta] : nullptr);
-    if (a.t4 || !kChunk) {
-        ntt_run(a, npoly, false, s);
-        return;
-    }
-    // past the four-step tables: one polynomial per launch pair, so its intermediate (beta n words,
-    // 128 MiB at 2^20 x 16) is read back by pass B from the 256 MiB Infinity Cache
-    const u64 N = 1ULL << (logn + logbeta);
-    for (int p = 0; p < npoly; p++) {
-        NttArgs b = a;
-        b.in = coef + (u64)p * coef_stride;
-        b.out = out + (u64)p * N;
-        ntt_run(b, 1, false, s);
-    }
+    ntt_run(a, npoly, false, s);
 }
 
 void launch_interpolate(const u64* evals, u64 in_stride, u64* out, u64 out_stride, u64* scratch, int npoly, int logn,
