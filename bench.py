@@ -166,8 +166,10 @@ class Exchange:
             return
         with torch.cuda.stream(stream):
             w = op(*args, async_op=True, **kw)
-        while not w.is_completed():
+        while not w.is_completed():  # also true once the collective has failed
             time.sleep(2e-5)
+        with torch.cuda.stream(stream):
+            w.wait()  # raises a failed collective's error; the stream wait it adds is already satisfied
 
     def _copy(self, stream, dst, src):
         import torch
