@@ -369,7 +369,7 @@ def pipelined_steps(submit_fn, collect_fn, batches, depth=2, ex=None, packed=Non
     return out
 
 
-def config5(prover, gpu, batch=4, calls=8, depth=4):
+def config5(prover, gpu, batch=4, calls=12, depth=6):
     """side measurement of BASELINE configs[4]: 2^20-step trace, blowup 16, 96-bit class options
     (quadratic extension, 24 queries, grinding 4), batches of `batch` proofs per call on this GPU,
     `depth` calls in flight; the trace LDE (7 columns, one proof) against the HBM roofline with
