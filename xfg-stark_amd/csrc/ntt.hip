@@ -553,6 +553,7 @@ __global__ __launch_bounds__(256, 4) void ntt_pass_a_cos2(NttArgs a) {
 }
 
 // ---------------------------------------------------------------- pass A, R = 1024, no four-step table
+constexpr bool kTab4 = true;
 // Forward pass A of the LDEs past the four-step tables (configs[4]: 2^20 x 16, R = C = 1024, radix
 // 32 x 32): one (8-column tile, poly, coset) per 256-thread block, a tile's cosets side by side on one
 // XCD (xcd_block_coset: the coefficient tile comes from HBM once, from L2 beta - 1 times). The coset
@@ -569,6 +570,7 @@ __global__ __launch_bounds__(256, 3) void ntt_pass_a_r1024(NttArgs a) {
     extern __shared__ u64 lds[];
     u32* tile = reinterpret_cast<u32*>(lds);
     u64* comb = lds + (TC * PITCH + 1) / 2;
+    u64* pre2 = comb + R;  // [r][seq]: kTab4 first-step factors of this tile's 8 columns
     int bx, by;
     xcd_block_coset(a.logbeta, bx, by);
     const int pt = by, col0 = bx * TC, poly = pt >> a.logbeta, t = pt & ((1 << a.logbeta) - 1);
@@ -577,40 +579,62 @@ __global__ __launch_bounds__(256, 3) void ntt_pass_a_r1024(NttArgs a) {
     const u64* comb_t = a.pt + R + (1 << a.logC) + ((u64)R << a.logbeta) + ((u64)t << LOGR);  // [r][k]
     for (int i = threadIdx.x; i < R; i += NT) comb[i] = comb_t[i];
     // (read only by the second step, behind pass_dft_split's first barrier)
-    const auto rin = buf_rsrc(a.in + (u64)poly * a.in_stride + col0);
-    auto ldg = [&](int seq, int j, int o) -> u64 {
-        return gl_mul(buf_ld(rin, (((u32)j << a.logC) + seq) * 8, ((u32)o << a.logC) * 8), pre[o]);
-    };
-    // four-step twiddle of output k1 = base + 32 q of column j2 (base < 32: the last step's group):
-    // 7^j2 w_N^(j2 (t + beta k1)) = [7^j2 w_N^(j2 t)] [w_n^(j2 base)] w_n^(32 j2 q), the two seed factors and
-    // the step read from small L2-resident tables (pass_tables_kernel; a gather from the 2^24-entry master
-    // table fetched a 128 B line for every 8 B it used)
+    // four-step factor of output k1 = base + 32 q of column j2: 7^j2 w_N^(j2 (t + beta k1)) =
+    // s_t(j2) w_n^(j2 k1), s_t(j2) = 7^j2 w_N^(j2 t), both from tables appended to the pass tables
+    // (pass_tables_kernel): [t][j2] and the t-independent [k1][j2] (8 MiB at n = 2^20)
     const u64* xt = a.pt + R + (1 << a.logC) + ((u64)(2 * R) << a.logbeta);
     const u64* seed_t = xt + ((u64)t << 10);
-    const u64* seed_b = xt + ((u64)1 << (10 + a.logbeta));
-    const u64* step_t = seed_b + (32 << 10);
-    u64 p7 = 0, w0 = 0, stp = 0;
-    auto pf = [&](int, int seq, int base, int) {
-        const int j2 = col0 + seq;
-        p7 = seed_t[j2];
-        w0 = seed_b[(base << 10) + j2];
-        stp = step_t[j2];
-    };
+    const u64* t4 = xt + ((u64)1 << (10 + a.logbeta));
+    const auto rin = buf_rsrc(a.in + (u64)poly * a.in_stride + col0);
     u64* y = a.y + (u64)pt * n;
-    auto stg = [&](int, int seq, int base, int stride, u64* v) {
-        u64 w = gl_mul(p7, w0);
+    if constexpr (kTab4) {
+        // s_t(j2) does not depend on the output row: it rides on the first step's element factor,
+        // pre2[o][seq] = g_t^(32 o) s_t(col0 + seq) (one multiply per thread per block), and each output
+        // takes one multiply by its [k1][j2] table entry -- instead of a running product (two per output).
+        // The 16 cosets of a column tile run back to back on one XCD, so their 64 KiB table slice is
+        // read from its L2.
+        // (the first step's element r of group j is row j + 32 r: o = 32 r)
+        pre2[threadIdx.x] = gl_mul(pre[(threadIdx.x >> 3) << 5], seed_t[col0 + (threadIdx.x & 7)]);
+        __syncthreads();
+        auto ldg = [&](int seq, int j, int o) -> u64 {
+            return gl_mul(buf_ld(rin, (((u32)j << a.logC) + seq) * 8, ((u32)o << a.logC) * 8), pre2[(o >> 5) * TC + seq]);
+        };
+        auto stg = [&](int, int seq, int base, int stride, u64* v) {
+            const u64* tk = t4 + ((u64)base << 10) + col0 + seq;
 #pragma unroll
-        for (int r = 0; r < RR; r++) {
-            v[r] = gl_mul(v[r], w);
-            if (r + 1 < RR) w = gl_mul(w, stp);
-        }
-        const u64 c2 = (u64)(col0 + seq) & ~1ULL;
-        store_pairs<RR>(v, [&](int r) { return y + ((u64)(base + r * stride) << a.logC) + c2; });
-    };
-    pass_dft_split<LOGR, LOGE, false, true, NT, decltype(ldg), decltype(stg), decltype(pf), true>(tile, logTC, comb,
-                                                                                                ldg, stg, pf);
+            for (int r = 0; r < RR; r++) v[r] = gl_mul(v[r], tk[(u64)(r * stride) << 10]);
+            const u64 c2 = (u64)(col0 + seq) & ~1ULL;
+            store_pairs<RR>(v, [&](int r) { return y + ((u64)(base + r * stride) << a.logC) + c2; });
+        };
+        pass_dft_split<LOGR, LOGE, false, true, NT, decltype(ldg), decltype(stg), NoPf, true>(tile, logTC, comb, ldg,
+                                                                                           stg, NoPf{});
+    } else {
+        auto ldg = [&](int seq, int j, int o) -> u64 {
+            return gl_mul(buf_ld(rin, (((u32)j << a.logC) + seq) * 8, ((u32)o << a.logC) * 8), pre[o]);
+        };
+        // running product: seed s_t(j2) w_n^(j2 base), step w_n^(32 j2) (rows base and 32 of the table)
+        u64 p7 = 0, w0 = 0, stp = 0;
+        auto pf = [&](int, int seq, int base, int) {
+            const int j2 = col0 + seq;
+            p7 = seed_t[j2];
+            w0 = t4[(base << 10) + j2];
+            stp = t4[(32 << 10) + j2];
+        };
+        auto stg = [&](int, int seq, int base, int stride, u64* v) {
+            u64 w = gl_mul(p7, w0);
+#pragma unroll
+            for (int r = 0; r < RR; r++) {
+                v[r] = gl_mul(v[r], w);
+                if (r + 1 < RR) w = gl_mul(w, stp);
+            }
+            const u64 c2 = (u64)(col0 + seq) & ~1ULL;
+            store_pairs<RR>(v, [&](int r) { return y + ((u64)(base + r * stride) << a.logC) + c2; });
+        };
+        pass_dft_split<LOGR, LOGE, false, true, NT, decltype(ldg), decltype(stg), decltype(pf), true>(tile, logTC, comb,
+                                                                                                    ldg, stg, pf);
+    }
 }
-size_t pass_a_r1024_lds() { return (size_t)((8 * split_pitch(1024, 5, 3) + 1) / 2 + 1024) * sizeof(u64); }
+size_t pass_a_r1024_lds() { return (size_t)((8 * split_pitch(1024, 5, 3) + 1) / 2 + 1024 + 256) * sizeof(u64); }
 
 // Forward pass B of the same LDEs: row DFTs of C = 1024 (radix 32 x 32), one 8-row tile per 256-thread
 // block with the exchange in 32-bit halves (three blocks per CU), canonical outputs stored as row
@@ -972,20 +996,17 @@ __global__ void pass_tables_kernel(u64* out, int logn, int logbeta, int logR, in
         const u64 t = q >> 10, r = (q >> 5) & 31, k = q & 31;
         const u64 g = gl_mul(T.pow7[r << logC], tw_get(T, logR + logbeta, (t * r) & ((1ULL << (logR + logbeta)) - 1), false));
         out[i] = gl_mul(tw_get(T, logR, r * k, false), g);
-    } else if (!inv && logR == 10 && i < R + C + 2 * (R << logbeta) + (C << logbeta) + 33 * C) {
-        // ntt_pass_a_r1024's four-step running-product seeds and step, from small tables instead of
-        // gathers from the master table: [t][j2] 7^j2 w_N^(j2 t), [b][j2] w_n^(j2 b) (b < 32), [j2] w_n^(32 j2)
+    } else if (!inv && logR == 10 && i < R + C + 2 * (R << logbeta) + (C << logbeta) + R * C) {
+        // ntt_pass_a_r1024's four-step factors: [t][j2] 7^j2 w_N^(j2 t) (t < beta, j2 < C) and the
+        // t-independent four-step table [k1][j2] w_n^(j2 k1) (R x C)
         const u64 q = i - R - C - 2 * (R << logbeta);
         const int logn = logR + logC, logN = logn + logbeta;
         if (q < (C << logbeta)) {
             const u64 t = q >> logC, j2 = q & (C - 1);
             out[i] = gl_mul(T.pow7[j2], tw_get(T, logN, (j2 * t) & ((1ULL << logN) - 1), false));
-        } else if (q < (C << logbeta) + 32 * C) {
-            const u64 b = (q - (C << logbeta)) >> logC, j2 = q & (C - 1);
-            out[i] = tw_get(T, logn, (j2 * b) & ((1ULL << logn) - 1), false);
         } else {
-            const u64 j2 = q & (C - 1);
-            out[i] = tw_get(T, logn, (32 * j2) & ((1ULL << logn) - 1), false);
+            const u64 k1 = (q - (C << logbeta)) >> logC, j2 = q & (C - 1);
+            out[i] = tw_get(T, logn, (j2 * k1) & ((1ULL << logn) - 1), false);
         }
     } else if (!inv && logR == 8 && logbeta >= 2) {
         // ntt_pass_a_cos2: [t][r][k] = w_R^(r k) 7^(C r) w_(beta R)^(t r), then [c][r] = 7^(16 C r) w_(16 beta)^(c r)
@@ -1004,7 +1025,7 @@ __global__ void pass_tables_kernel(u64* out, int logn, int logbeta, int logR, in
 // entries of the ntt_pass_a_cos2 tables appended to the forward pass tables (R = 256, beta >= 4), or of
 // the ntt_pass_a_r1024 tables (R = 1024)
 static u64 cos2_extra(int logR, int logC, int logbeta) {
-    if (logbeta >= 0 && logR == 10) return (1ULL << (logR + logbeta)) + (1ULL << (logC + logbeta)) + (33ULL << logC);
+    if (logbeta >= 0 && logR == 10 && logC == 10) return (1ULL << (logR + logbeta)) + (1ULL << (logC + logbeta)) + (1ULL << (logR + logC));
     return (logbeta >= 0 && logR == 8 && logbeta >= 2) ? ((1ULL << (logR + logbeta)) + (16ULL << (logbeta - 2))) : 0;
 }
 u64 pass_tables_size(int logn, int logbeta) {
