@@ -554,6 +554,7 @@ __global__ __launch_bounds__(256, 4) void ntt_pass_a_cos2(NttArgs a) {
 
 // ---------------------------------------------------------------- pass A, R = 1024, no four-step table
 constexpr bool kTab4 = true;
+constexpr bool kTileMajor = true;
 // Forward pass A of the LDEs past the four-step tables (configs[4]: 2^20 x 16, R = C = 1024, radix
 // 32 x 32): one (8-column tile, poly, coset) per 256-thread block, a tile's cosets side by side on one
 // XCD (xcd_block_coset: the coefficient tile comes from HBM once, from L2 beta - 1 times). The coset
@@ -587,6 +588,13 @@ __global__ __launch_bounds__(256, 3) void ntt_pass_a_r1024(NttArgs a) {
     const u64* t4 = xt + ((u64)1 << (10 + a.logbeta));
     const auto rin = buf_rsrc(a.in + (u64)poly * a.in_stride + col0);
     u64* y = a.y + (u64)pt * n;
+    // the intermediate element (k1, j2): tile-major (kTileMajor: the block's 8 columns x 1024 rows are one
+    // contiguous 64 KiB run, so rows k1, k1 + 1 of a column pair -- lanes of one store instruction --
+    // fill whole 128 B lines) or row-major [k1][j2]
+    auto yat = [&](int k1, int seq) -> u64* {
+        const int c2 = seq & ~1;
+        return kTileMajor ? y + ((u64)bx << 13) + ((u64)k1 << 3) + c2 : y + ((u64)k1 << a.logC) + col0 + c2;
+    };
     if constexpr (kTab4) {
         // s_t(j2) does not depend on the output row: it rides on the first step's element factor,
         // pre2[o][seq] = g_t^(32 o) s_t(col0 + seq) (one multiply per thread per block), and each output
@@ -603,8 +611,7 @@ __global__ __launch_bounds__(256, 3) void ntt_pass_a_r1024(NttArgs a) {
             const u64* tk = t4 + ((u64)base << 10) + col0 + seq;
 #pragma unroll
             for (int r = 0; r < RR; r++) v[r] = gl_mul(v[r], tk[(u64)(r * stride) << 10]);
-            const u64 c2 = (u64)(col0 + seq) & ~1ULL;
-            store_pairs<RR>(v, [&](int r) { return y + ((u64)(base + r * stride) << a.logC) + c2; });
+            store_pairs<RR>(v, [&](int r) { return yat(base + r * stride, seq); });
         };
         pass_dft_split<LOGR, LOGE, false, true, NT, decltype(ldg), decltype(stg), NoPf, true>(tile, logTC, comb, ldg,
                                                                                            stg, NoPf{});
@@ -627,8 +634,7 @@ __global__ __launch_bounds__(256, 3) void ntt_pass_a_r1024(NttArgs a) {
                 v[r] = gl_mul(v[r], w);
                 if (r + 1 < RR) w = gl_mul(w, stp);
             }
-            const u64 c2 = (u64)(col0 + seq) & ~1ULL;
-            store_pairs<RR>(v, [&](int r) { return y + ((u64)(base + r * stride) << a.logC) + c2; });
+            store_pairs<RR>(v, [&](int r) { return yat(base + r * stride, seq); });
         };
         pass_dft_split<LOGR, LOGE, false, true, NT, decltype(ldg), decltype(stg), decltype(pf), true>(tile, logTC, comb,
                                                                                                     ldg, stg, pf);
@@ -650,11 +656,20 @@ __global__ __launch_bounds__(256, 3) void ntt_pass_b_r1024(NttArgs a) {
     const int pt = by, k10 = bx * TR;
     const u64 n = 1ULL << a.logn;
     for (int i = threadIdx.x; i < C; i += NT) ltw[i] = a.pt[(1 << a.logR) + i];
-    const int seq0 = threadIdx.x / G1, j0 = threadIdx.x % G1;
-    const u64* y = a.y + (u64)pt * n + ((u64)(k10 + seq0) << LOGC) + j0;
+    // this thread's first-step group: rows fastest over a tile-major intermediate (8 rows x 8 columns of
+    // one column tile = 512 contiguous bytes per load instruction), columns fastest over a row-major one
+    const int seq0 = kTileMajor ? threadIdx.x & (TR - 1) : threadIdx.x / G1;
+    const int j0 = kTileMajor ? threadIdx.x >> logTR : threadIdx.x % G1;
     u64 yv[R1];
+    if constexpr (kTileMajor) {
+        const u64* y = a.y + (u64)pt * n + ((u64)(j0 >> 3) << 13) + ((u64)(k10 + seq0) << 3) + (j0 & 7);
 #pragma unroll
-    for (int r = 0; r < R1; r++) yv[r] = y[r * G1];
+        for (int r = 0; r < R1; r++) yv[r] = y[(u64)r << 15];  // column j0 + 32 r: 4 tiles further
+    } else {
+        const u64* y = a.y + (u64)pt * n + ((u64)(k10 + seq0) << LOGC) + j0;
+#pragma unroll
+        for (int r = 0; r < R1; r++) yv[r] = y[r * G1];
+    }
     __syncthreads();
     auto ldg = [&](int, int, int o) -> u64 { return yv[o / G1]; };
     u64* out = a.out + (u64)pt * n + k10;
@@ -663,7 +678,7 @@ __global__ __launch_bounds__(256, 3) void ntt_pass_b_r1024(NttArgs a) {
         for (int r = 0; r < RR; r++) v[r] = canon(v[r]);
         store_pairs<RR>(v, [&](int r) { return out + (seq & ~1) + ((u64)(base + r * stride) << a.logR); });
     };
-    pass_dft_split<LOGC, LOGE, false, false, NT>(tile, logTR, ltw, ldg, stg, NoPf{});
+    pass_dft_split<LOGC, LOGE, false, kTileMajor, NT>(tile, logTR, ltw, ldg, stg, NoPf{});
 }
 size_t pass_b_r1024_lds() { return (size_t)((8 * split_pitch(1024, 5, 3) + 1) / 2 + 1024) * sizeof(u64); }
 
