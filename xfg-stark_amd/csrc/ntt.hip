@@ -553,98 +553,64 @@ __global__ __launch_bounds__(256, 4) void ntt_pass_a_cos2(NttArgs a) {
 }
 
 // ---------------------------------------------------------------- pass A, R = 1024, no four-step table
-constexpr bool kTab4 = true;
-constexpr bool kTileMajor = true;
 // Forward pass A of the LDEs past the four-step tables (configs[4]: 2^20 x 16, R = C = 1024, radix
 // 32 x 32): one (8-column tile, poly, coset) per 256-thread block, a tile's cosets side by side on one
-// XCD (xcd_block_coset: the coefficient tile comes from HBM once, from L2 beta - 1 times). The coset
-// pre-factor g_t^j1 (g_t = 7^C w_(beta R)^t), j1 = j0 + 32 r, splits into an element factor g_t^(32 r)
-// -- the same for every lane, read from the pass table by scalar loads -- and a group factor g_t^j0
-// that rides on the second step's twiddle: a per-coset [r][k] table w_1024^(r k) g_t^r in LDS. No
-// per-lane pre-factor loads, so the first step's loads hold 64 VGPRs, not 128. The exchange between
-// the two radix-32 steps goes through the LDS tile in 32-bit halves (pass_dft_split: 42 KiB per
-// block, three blocks per CU); the four-step twiddles are running products applied at the store,
-// which writes column pairs (store_pairs).
+// XCD (xcd_block_coset: the coefficient tile comes from HBM once, from L2 beta - 1 times).
+//  * Coset pre-factor g_t^j1 (g_t = 7^C w_(beta R)^t), j1 = j0 + 32 r: the group factor g_t^j0 rides on
+//    the second step's twiddle (a per-coset [r][k] table w_1024^(r k) g_t^r in LDS), the element factor
+//    g_t^(32 r) on the first step's loads.
+//  * Four-step factor of output k1 of column j2: 7^j2 w_N^(j2 (t + beta k1)) = s_t(j2) w_n^(j2 k1). s_t(j2)
+//    = 7^j2 w_N^(j2 t) does not depend on k1, so it joins the element factor (pre2[r][seq] = g_t^(32 r)
+//    s_t(col0 + seq), one multiply per thread per block), and every output takes one multiply by its
+//    entry of the t-independent [k1][j2] table (8 MiB, appended to the pass tables; a column tile's 16
+//    cosets read its 64 KiB slice from one L2) -- not a running product (two multiplies per output).
+//  * The exchange between the two radix-32 steps goes through the LDS tile in 32-bit halves
+//    (pass_dft_split at split_pitch: 42 KiB per block, three blocks per CU, no bank conflicts).
+//  * The intermediate is tile-major: the block's 8 columns x 1024 rows are one contiguous 64 KiB run,
+//    so rows k1, k1 + 1 of a column pair -- lanes of one store_pairs instruction -- fill whole 128 B
+//    lines (row-major, each line was half-written by two blocks 16 launches apart: 15 % more write
+//    requests).
 __global__ __launch_bounds__(256, 3) void ntt_pass_a_r1024(NttArgs a) {
     constexpr int LOGR = 10, LOGE = 5, NT = 256, R = 1 << LOGR, RR = 32, logTC = 3, TC = 1 << logTC;
     constexpr int PITCH = split_pitch(R, LOGE, NT_LOG2(NT) + LOGE - LOGR);
     extern __shared__ u64 lds[];
     u32* tile = reinterpret_cast<u32*>(lds);
     u64* comb = lds + (TC * PITCH + 1) / 2;
-    u64* pre2 = comb + R;  // [r][seq]: kTab4 first-step factors of this tile's 8 columns
+    u64* pre2 = comb + R;  // [r][seq]: first-step factors of this tile's 8 columns
     int bx, by;
     xcd_block_coset(a.logbeta, bx, by);
     const int pt = by, col0 = bx * TC, poly = pt >> a.logbeta, t = pt & ((1 << a.logbeta) - 1);
     const u64 n = 1ULL << a.logn;
     const u64* pre = a.pt + R + (1 << a.logC) + (u64)t * R;                                     // g_t^j1
     const u64* comb_t = a.pt + R + (1 << a.logC) + ((u64)R << a.logbeta) + ((u64)t << LOGR);  // [r][k]
-    for (int i = threadIdx.x; i < R; i += NT) comb[i] = comb_t[i];
-    // (read only by the second step, behind pass_dft_split's first barrier)
-    // four-step factor of output k1 = base + 32 q of column j2: 7^j2 w_N^(j2 (t + beta k1)) =
-    // s_t(j2) w_n^(j2 k1), s_t(j2) = 7^j2 w_N^(j2 t), both from tables appended to the pass tables
-    // (pass_tables_kernel): [t][j2] and the t-independent [k1][j2] (8 MiB at n = 2^20)
     const u64* xt = a.pt + R + (1 << a.logC) + ((u64)(2 * R) << a.logbeta);
-    const u64* seed_t = xt + ((u64)t << 10);
-    const u64* t4 = xt + ((u64)1 << (10 + a.logbeta));
+    const u64* seed_t = xt + ((u64)t << 10);                   // [t][j2] s_t(j2)
+    const u64* t4 = xt + ((u64)1 << (10 + a.logbeta));          // [k1][j2] w_n^(j2 k1)
+    for (int i = threadIdx.x; i < R; i += NT) comb[i] = comb_t[i];
+    // (comb is read only by the second step, behind pass_dft_split's first barrier; the first step's
+    // element r of group j is row j + 32 r)
+    pre2[threadIdx.x] = gl_mul(pre[(threadIdx.x >> 3) << 5], seed_t[col0 + (threadIdx.x & 7)]);
+    __syncthreads();
     const auto rin = buf_rsrc(a.in + (u64)poly * a.in_stride + col0);
-    u64* y = a.y + (u64)pt * n;
-    // the intermediate element (k1, j2): tile-major (kTileMajor: the block's 8 columns x 1024 rows are one
-    // contiguous 64 KiB run, so rows k1, k1 + 1 of a column pair -- lanes of one store instruction --
-    // fill whole 128 B lines) or row-major [k1][j2]
-    auto yat = [&](int k1, int seq) -> u64* {
-        const int c2 = seq & ~1;
-        return kTileMajor ? y + ((u64)bx << 13) + ((u64)k1 << 3) + c2 : y + ((u64)k1 << a.logC) + col0 + c2;
+    auto ldg = [&](int seq, int j, int o) -> u64 {
+        return gl_mul(buf_ld(rin, (((u32)j << a.logC) + seq) * 8, ((u32)o << a.logC) * 8), pre2[(o >> 5) * TC + seq]);
     };
-    if constexpr (kTab4) {
-        // s_t(j2) does not depend on the output row: it rides on the first step's element factor,
-        // pre2[o][seq] = g_t^(32 o) s_t(col0 + seq) (one multiply per thread per block), and each output
-        // takes one multiply by its [k1][j2] table entry -- instead of a running product (two per output).
-        // The 16 cosets of a column tile run back to back on one XCD, so their 64 KiB table slice is
-        // read from its L2.
-        // (the first step's element r of group j is row j + 32 r: o = 32 r)
-        pre2[threadIdx.x] = gl_mul(pre[(threadIdx.x >> 3) << 5], seed_t[col0 + (threadIdx.x & 7)]);
-        __syncthreads();
-        auto ldg = [&](int seq, int j, int o) -> u64 {
-            return gl_mul(buf_ld(rin, (((u32)j << a.logC) + seq) * 8, ((u32)o << a.logC) * 8), pre2[(o >> 5) * TC + seq]);
-        };
-        auto stg = [&](int, int seq, int base, int stride, u64* v) {
-            const u64* tk = t4 + ((u64)base << 10) + col0 + seq;
+    u64* ytile = a.y + (u64)pt * n + ((u64)bx << 13);  // tile-major intermediate: [tile][k1][8]
+    auto stg = [&](int, int seq, int base, int stride, u64* v) {
+        const u64* tk = t4 + ((u64)base << 10) + col0 + seq;
 #pragma unroll
-            for (int r = 0; r < RR; r++) v[r] = gl_mul(v[r], tk[(u64)(r * stride) << 10]);
-            store_pairs<RR>(v, [&](int r) { return yat(base + r * stride, seq); });
-        };
-        pass_dft_split<LOGR, LOGE, false, true, NT, decltype(ldg), decltype(stg), NoPf, true>(tile, logTC, comb, ldg,
-                                                                                           stg, NoPf{});
-    } else {
-        auto ldg = [&](int seq, int j, int o) -> u64 {
-            return gl_mul(buf_ld(rin, (((u32)j << a.logC) + seq) * 8, ((u32)o << a.logC) * 8), pre[o]);
-        };
-        // running product: seed s_t(j2) w_n^(j2 base), step w_n^(32 j2) (rows base and 32 of the table)
-        u64 p7 = 0, w0 = 0, stp = 0;
-        auto pf = [&](int, int seq, int base, int) {
-            const int j2 = col0 + seq;
-            p7 = seed_t[j2];
-            w0 = t4[(base << 10) + j2];
-            stp = t4[(32 << 10) + j2];
-        };
-        auto stg = [&](int, int seq, int base, int stride, u64* v) {
-            u64 w = gl_mul(p7, w0);
-#pragma unroll
-            for (int r = 0; r < RR; r++) {
-                v[r] = gl_mul(v[r], w);
-                if (r + 1 < RR) w = gl_mul(w, stp);
-            }
-            store_pairs<RR>(v, [&](int r) { return yat(base + r * stride, seq); });
-        };
-        pass_dft_split<LOGR, LOGE, false, true, NT, decltype(ldg), decltype(stg), decltype(pf), true>(tile, logTC, comb,
-                                                                                                    ldg, stg, pf);
-    }
+        for (int r = 0; r < RR; r++) v[r] = gl_mul(v[r], tk[(u64)(r * stride) << 10]);
+        store_pairs<RR>(v, [&](int r) { return ytile + ((u64)(base + r * stride) << 3) + (seq & ~1); });
+    };
+    pass_dft_split<LOGR, LOGE, false, true, NT, decltype(ldg), decltype(stg), NoPf, true>(tile, logTC, comb, ldg, stg,
+                                                                                       NoPf{});
 }
 size_t pass_a_r1024_lds() { return (size_t)((8 * split_pitch(1024, 5, 3) + 1) / 2 + 1024 + 256) * sizeof(u64); }
 
 // Forward pass B of the same LDEs: row DFTs of C = 1024 (radix 32 x 32), one 8-row tile per 256-thread
-// block with the exchange in 32-bit halves (three blocks per CU), canonical outputs stored as row
-// pairs (store_pairs) into the coset-major LDE
+// block with the exchange in 32-bit halves (three blocks per CU). The first step walks the tile-major
+// intermediate rows fastest (8 rows x 8 columns of one column tile = 512 contiguous bytes per load
+// instruction); canonical outputs are stored as row pairs (store_pairs) into the coset-major LDE.
 __global__ __launch_bounds__(256, 3) void ntt_pass_b_r1024(NttArgs a) {
     constexpr int LOGC = 10, LOGE = 5, NT = 256, C = 1 << LOGC, R1 = 32, G1 = C / R1, RR = 32, logTR = 3;
     constexpr int TR = 1 << logTR, PITCH = split_pitch(C, LOGE, logTR);
@@ -656,20 +622,12 @@ __global__ __launch_bounds__(256, 3) void ntt_pass_b_r1024(NttArgs a) {
     const int pt = by, k10 = bx * TR;
     const u64 n = 1ULL << a.logn;
     for (int i = threadIdx.x; i < C; i += NT) ltw[i] = a.pt[(1 << a.logR) + i];
-    // this thread's first-step group: rows fastest over a tile-major intermediate (8 rows x 8 columns of
-    // one column tile = 512 contiguous bytes per load instruction), columns fastest over a row-major one
-    const int seq0 = kTileMajor ? threadIdx.x & (TR - 1) : threadIdx.x / G1;
-    const int j0 = kTileMajor ? threadIdx.x >> logTR : threadIdx.x % G1;
+    // this thread's first-step group (stockham, SEQ_FAST): row seq0 of the tile, columns j0 + 32 r
+    const int seq0 = threadIdx.x & (TR - 1), j0 = threadIdx.x >> logTR;
+    const u64* y = a.y + (u64)pt * n + ((u64)(j0 >> 3) << 13) + ((u64)(k10 + seq0) << 3) + (j0 & 7);
     u64 yv[R1];
-    if constexpr (kTileMajor) {
-        const u64* y = a.y + (u64)pt * n + ((u64)(j0 >> 3) << 13) + ((u64)(k10 + seq0) << 3) + (j0 & 7);
 #pragma unroll
-        for (int r = 0; r < R1; r++) yv[r] = y[(u64)r << 15];  // column j0 + 32 r: 4 tiles further
-    } else {
-        const u64* y = a.y + (u64)pt * n + ((u64)(k10 + seq0) << LOGC) + j0;
-#pragma unroll
-        for (int r = 0; r < R1; r++) yv[r] = y[r * G1];
-    }
+    for (int r = 0; r < R1; r++) yv[r] = y[(u64)r << 15];  // column j0 + 32 r: 4 tiles further
     __syncthreads();
     auto ldg = [&](int, int, int o) -> u64 { return yv[o / G1]; };
     u64* out = a.out + (u64)pt * n + k10;
@@ -678,7 +636,7 @@ __global__ __launch_bounds__(256, 3) void ntt_pass_b_r1024(NttArgs a) {
         for (int r = 0; r < RR; r++) v[r] = canon(v[r]);
         store_pairs<RR>(v, [&](int r) { return out + (seq & ~1) + ((u64)(base + r * stride) << a.logR); });
     };
-    pass_dft_split<LOGC, LOGE, false, kTileMajor, NT>(tile, logTR, ltw, ldg, stg, NoPf{});
+    pass_dft_split<LOGC, LOGE, false, true, NT>(tile, logTR, ltw, ldg, stg, NoPf{});
 }
 size_t pass_b_r1024_lds() { return (size_t)((8 * split_pitch(1024, 5, 3) + 1) / 2 + 1024) * sizeof(u64); }
 

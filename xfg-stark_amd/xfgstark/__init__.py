@@ -9,6 +9,7 @@ without a GPU the prover constructor raises.
 import ctypes as C
 import mmap
 import os
+import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _PKG = os.path.dirname(_HERE)
@@ -447,7 +448,7 @@ class PendingBatch:
     def __del__(self):
         # the workers write into this batch's buffers: never release them before the batch is done;
         # a batch that was waited for but never consumed returns its buffer to the pool
-        if getattr(self._p, "_ctx", None):
+        if not sys.is_finalizing() and getattr(self._p, "_ctx", None):
             if self._res is None and not hasattr(self, "_wst"):
                 _lib.xfg_batch_wait(self._p._ctx, self._t)
             self._release()
@@ -477,7 +478,10 @@ class XfgBurnMintProver:
             self._ctx = None
 
     def __del__(self):
-        self.close()
+        # at interpreter exit the module globals (and the HIP runtime) may already be gone; process
+        # teardown releases the device buffers, so only collect contexts dropped while running
+        if not sys.is_finalizing():
+            self.close()
 
     def _err(self, st):
         buf = C.create_string_buffer(1024)
