@@ -1,5 +1,5 @@
 """Multi-GPU path on CPU: bench.py's exchange step (bench.Exchange + bench.pipelined_steps) over
-torch.distributed gloo with world_size 2 and 4.
+torch.distributed gloo with world_size 2, 4 and 8 (the driver's 8-GPU shape).
 
 Rank 0 holds the packed burn inputs; each step's shard is scattered by its own collective, every
 rank "proves" its shard into a fixed-size exchange record (here: the product's host marshalling,
@@ -113,6 +113,7 @@ def _run(world, per, **kw):
     (2, 2, 5, 3, 2),
     (4, 2, 4, 2, 3),   # four ranks
     (4, 1, 9, 2, 3),   # more steps than send records and receive slots
+    (8, 2, 7, 2, 3),   # eight ranks, as on the driver's 8-GPU node
 ])
 def test_exchange_gloo(world, per, steps, depth, lookahead):
     import synthetic
