@@ -30,9 +30,11 @@ struct DeepParams {
 // 7^j2 w_N^(j2 (t + beta k1)) at [t][k1][j2], inv[logn] holds w_n^-(j2 k1) / n at [k1][j2];
 // nullptr -> the kernels form them as running products
 constexpr int FOURSTEP_MAX_LOG = 22;
-// forward sizes past FOURSTEP_MAX_LOG (configs[4]: 2^20 x 16 = 2^24 points, a 128 MB table) keep the
-// running-product four-step twiddles but still get the small per-size pass tables (w_R^i, w_C^i and
-// the coset pre-factors, R + C + beta R entries) as one contiguous block: pass_fwd[logn][logbeta]
+// forward sizes past FOURSTEP_MAX_LOG (configs[4]: 2^20 x 16 = 2^24 points, where a full table would
+// be 128 MB) get no beta n table, only the per-size pass tables as one contiguous block,
+// pass_fwd[logn][logbeta]: w_R^i, w_C^i and the coset pre-factors (R + C + beta R entries); at
+// R = C = 1024 also the per-coset [r][k] and [t][j2] factors and the coset-independent [k1][j2]
+// four-step table (8 MiB, ntt_pass_a_r1024); other sizes keep running-product four-step twiddles
 constexpr int PASS_MAX_LOG = 24;
 struct FourStep {
     const u64* fwd[FOURSTEP_MAX_LOG + 1][5] = {};

@@ -1041,8 +1041,9 @@ static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
     //   whole 128 B lines; pass B at C <= 1024 runs 512-thread blocks (8192 elements, <= 78 KiB, two
     //   blocks per CU: one block's barriers and loads hide behind the other's butterflies);
     // * radix-32 tiles: pass A 16 columns (512 threads at R = 1024, 256 at R = 512; the forward
-    //   R = 1024 pass of configs[4] 256 threads x 8 columns with the coset pre-factors read from L2 --
-    //   76 KiB of LDS, two blocks per CU), pass B 8192 elements (256 threads, two blocks per CU).
+    //   R = 1024 pass past the four-step tables at other C, e.g. 2^21, 256 threads x 8 columns with the
+    //   coset pre-factors read from L2 -- 76 KiB of LDS, two blocks per CU), pass B 8192 elements (256
+    //   threads, two blocks per CU). configs[4]'s 2^20 takes the dedicated R = C = 1024 passes below.
     const int eA = (a.logR >= 9 && a.logR <= 10 && a.logC >= 4) ? 5 : 4;
     const int eB = (a.logC >= 9 && a.logC <= 10 && a.logR >= 3) ? 5 : 4;
     const bool capA = a.logR >= 9 && a.logR <= 10 && a.logC >= 4, capB = a.logC >= 9 && a.logC <= 11 && a.logR >= 4;

@@ -414,9 +414,10 @@ static Tables tables_of(xfg_ctx* c) {
 }
 // four-step twiddle tables of the NTT sizes one (n, beta) proof uses: the forward LDE and the
 // inverse NTTs of sizes 8 .. 2n (trace, composition, FRI remainder). Sizes whose table would exceed
-// 2^FOURSTEP_MAX_LOG entries keep the running-product twiddles. Returns false when one is missing.
-// largest log2(n beta) with a forward four-step table (a 2^24-entry table for configs[4] measured
-// slower than the running-product twiddles)
+// 2^FOURSTEP_MAX_LOG entries get the per-size pass tables instead (at 2^20 with the n-entry [k1][j2]
+// table of ntt_pass_a_r1024: a full 2^24-entry table for configs[4] measured slower).
+// Returns false when one is missing.
+// largest log2(n beta) with a forward four-step table
 static int fwd_table_max_log() { return FOURSTEP_MAX_LOG; }
 static bool fourstep_ready(xfg_ctx* c, int logn, int logbeta) {
     const FourStep& f = c->tables.fs;
