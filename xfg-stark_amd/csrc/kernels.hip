@@ -973,4 +973,21 @@ void launch_gather_set(const GatherSet& g, const u64* idx, hipStream_t s) {
     XFG_CHECK_LAUNCH();
 }
 
+// one segment per blockIdx.y, grid-stride over its words
+__global__ void pack_kernel(PackSet p, u32* dst) {
+    const int k = blockIdx.y;
+    const u32* src = (const u32*)p.src[k];
+    u32* out = dst + p.off[k];
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < p.words[k]; i += (u64)gridDim.x * blockDim.x)
+        out[i] = src[i];
+}
+void launch_pack(const PackSet& p, void* dst, hipStream_t s) {
+    u64 most = 0;
+    for (int k = 0; k < p.nseg; k++) most = std::max(most, p.words[k]);
+    if (!most) return;
+    const unsigned bx = (unsigned)std::min<u64>(32, (most + 255) / 256);
+    hipLaunchKernelGGL(pack_kernel, dim3(bx, p.nseg), dim3(256), 0, s, p, (u32*)dst);
+    XFG_CHECK_LAUNCH();
+}
+
 }  // namespace xfg

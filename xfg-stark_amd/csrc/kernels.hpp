@@ -163,4 +163,14 @@ struct GatherSet {
 };
 void launch_gather_set(const GatherSet& g, const u64* idx, hipStream_t s);
 
+// contiguous device regions packed end to end into one block (segment k: words[k] 32-bit words
+// from src[k] to dst + off[k] words); dst may be device-mapped pinned host memory
+struct PackSet {
+    static constexpr int MAX = 12;
+    int nseg = 0;
+    const void* src[MAX];
+    u64 off[MAX], words[MAX];
+};
+void launch_pack(const PackSet& p, void* dst, hipStream_t s);
+
 }  // namespace xfg

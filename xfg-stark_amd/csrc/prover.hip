@@ -289,20 +289,19 @@ struct Lane {
     u64 lde_sets = 0, lde_polys = 0;
     DBuf<AirConst> air;
     DBuf<u64> coeffs, trace, coef, scratch, lde, ce, hcoef, hlde, zpts, partial, ood, carry, deep, f0, alpha7,
-        rem, gidx, gval, dn2, falpha;
-    DBuf<Digest> tnodes, hnodes, gdig, droots;
+        rem, dn2, falpha;
+    DBuf<Digest> tnodes, hnodes, droots;
     DBuf<DeepParams> dp;
     DBuf<DevCoin> dcoin;  // device-side transcript
     DBuf<int> dfail;
     std::vector<DBuf<u64>> flayer;
     std::vector<DBuf<Digest>> fnodes;
     // pinned host staging
-    HBuf<Digest> h_roots, h_gd;
-    HBuf<u64> h_co, h_ood, h_rem, h_dn2, h_idx, h_gv, h_falpha;
+    HBuf<Digest> h_gd;
+    HBuf<u64> h_idx, h_gv;
+    HBuf<unsigned char> h_xfer;  // the replay's inputs, written by launch_pack
     HBuf<AirConst> h_air;
     HBuf<DevCoin> h_coin;
-    HBuf<DeepParams> h_dp;
-    HBuf<int> h_fail;
     // host scratch of the opening plans and the serialiser, kept across units so steady-state
     // units neither allocate nor page-fault (their cost grew with the shared hosts' load)
     struct {
@@ -310,19 +309,18 @@ struct Lane {
         std::vector<LaneLayout> lay;
     } hs;
     void release() {
-        for (auto* b : {&h_roots, &h_gd}) b->release();
-        for (auto* b : {&h_co, &h_ood, &h_rem, &h_dn2, &h_idx, &h_gv, &h_falpha}) b->release();
+        h_gd.release();
+        for (auto* b : {&h_idx, &h_gv}) b->release();
+        h_xfer.release();
         h_air.release();
         h_coin.release();
-        h_dp.release();
-        h_fail.release();
         dcoin.release();
         dfail.release();
         air.release();
         for (auto* b : {&coeffs, &trace, &coef, &scratch, &lde, &ce, &hcoef, &hlde, &zpts, &partial, &ood,
-                        &carry, &deep, &f0, &alpha7, &rem, &gidx, &gval, &dn2, &falpha})
+                        &carry, &deep, &f0, &alpha7, &rem, &dn2, &falpha})
             b->release();
-        for (auto* b : {&tnodes, &hnodes, &gdig, &droots}) b->release();
+        for (auto* b : {&tnodes, &hnodes, &droots}) b->release();
         dp.release();
         for (auto& b : flayer) b.release();
         for (auto& b : fnodes) b.release();
@@ -567,16 +565,14 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     const u64 rem_len = N >> (3 * nl) >> logbeta;  // D_final / blowup
     c->rem.ensure((size_t)B * DE * std::max<u64>(rem_len, 1));
     {
-        // opening buffers sized by upper bounds once, so steady-state calls never re-allocate
-        // (hipFree / hipHostMalloc would serialise the device and the other lanes)
+        // opening buffers (pinned, device-mapped: the gathers read and write them directly) sized by
+        // upper bounds once, so steady-state calls never re-allocate (hipHostMalloc would serialise
+        // the device and the other lanes)
         const size_t q = o.q, depth = logn + logbeta;
         const size_t vals = (size_t)B * q * (7 + DE + 8 * DE * nl);
         size_t digs = (size_t)B * q * 2 * depth;
         for (unsigned l = 0; l < nl; l++) digs += (size_t)B * q * ilog2(D[l] / 8);
         const size_t opens = (size_t)B * q * 2 * 2 * 2 * beta;
-        c->gidx.ensure(vals + digs + (size_t)B * 2 * q);
-        c->gval.ensure(vals);
-        c->gdig.ensure(digs + opens);
         c->h_idx.ensure(vals + digs + (size_t)B * 2 * q);
         c->h_gv.ensure(vals);
         c->h_gd.ensure(digs + opens);
@@ -688,33 +684,53 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
                         c->flayer[l + 1].p, rows, T, B, DE, s);
     }
     ht.mark("chain_launch");
-    // transcript inputs for the host replay: trace / composition roots, OOD frame, FRI roots
-    Digest* roots = c->h_roots.ensure((size_t)(2 + nl) * B);  // [trace, composition, FRI 0..nl-1][B]
-    HIPCHK(hipMemcpyAsync(roots, c->droots.p, (size_t)(2 + nl) * B * sizeof(Digest), hipMemcpyDeviceToHost, s));
-    u64* ood = c->h_ood.ensure((size_t)B * 15 * DE);
-    HIPCHK(hipMemcpyAsync(ood, c->ood.p, (size_t)B * 15 * DE * 8, hipMemcpyDeviceToHost, s));
-    u64* co = c->h_co.ensure((size_t)B * 15 * DE);  // the device's draws, checked by the replay
-    HIPCHK(hipMemcpyAsync(co, c->coeffs.p, (size_t)B * 15 * DE * 8, hipMemcpyDeviceToHost, s));
-    DeepParams* dps = c->h_dp.ensure(B);
-    HIPCHK(hipMemcpyAsync(dps, c->dp.p, B * sizeof(DeepParams), hipMemcpyDeviceToHost, s));
-    const Digest* froots = roots + 2 * B;
-    u64* falpha = c->h_falpha.ensure((size_t)std::max(1u, nl) * B * DE);  // [layer][B][DE]
-    if (nl) HIPCHK(hipMemcpyAsync(falpha, c->falpha.p, (size_t)nl * B * DE * 8, hipMemcpyDeviceToHost, s));
-    int* ffail = c->h_fail.ensure(B);
-    HIPCHK(hipMemcpyAsync(ffail, c->dfail.p, B * sizeof(int), hipMemcpyDeviceToHost, s));
     // remainder: interpolate the last layer over 7*<w_D>, keep D/blowup coefficients
-    // (with no folding layer this is the DEEP polynomial's own coefficients)
-    u64* remh = c->h_rem.ensure((size_t)B * DE * rem_len);  // planes [b][c][rem_len]
+    // (with no folding layer this is the DEEP polynomial's own coefficients), planes [b][c][rem_len]
     if (nl > 0) {
         launch_interpolate(c->flayer[nl].p, D[nl], c->rem.p, rem_len, c->scratch.p, B * DE, (int)ilog2(D[nl]), true,
                            rem_len, T, s);
-        HIPCHK(hipMemcpyAsync(remh, c->rem.p, (size_t)B * DE * rem_len * 8, hipMemcpyDeviceToHost, s));
     } else {
-        HIPCHK(hipMemcpy2DAsync(remh, rem_len * 8, c->deep.p, n * 8, rem_len * 8, (size_t)B * DE, hipMemcpyDeviceToHost,
-                                s));
+        HIPCHK(hipMemcpy2DAsync(c->rem.p, rem_len * 8, c->deep.p, n * 8, rem_len * 8, (size_t)B * DE,
+                                hipMemcpyDeviceToDevice, s));
     }
-    u64* dn2h = c->h_dn2.ensure((size_t)B * DE);
-    HIPCHK(hipMemcpyAsync(dn2h, c->dn2.p, (size_t)B * DE * 8, hipMemcpyDeviceToHost, s));
+    // transcript inputs for the host replay (trace / composition / FRI roots, OOD frame, the device's
+    // draws, DEEP parameters, FRI alphas, rejections, remainder, DEEP degree check): one kernel packs
+    // them straight into the pinned host block (device-mapped, written with plain vector stores),
+    // visible to the host after the stream synchronisation below. As eight hipMemcpyAsync blits each
+    // could start ~0.2 ms after the previous one (rocprof, scripts/fri_timeline.sh: 1.7 ms of idle
+    // stream after the last FRI fold); as one larger copy the runtime takes the SDMA engine, whose
+    // dependency on the lane stream cost 17 % of the pipelined throughput (same box, lib_ab.sh)
+    PackSet pk;
+    u64 words = 0;
+    auto seg = [&](const void* src, size_t bytes) {
+        const u64 at = words;
+        pk.src[pk.nseg] = src;
+        pk.off[pk.nseg] = at;
+        pk.words[pk.nseg++] = bytes / 4;
+        words = (at + bytes / 4 + 63) & ~63ULL;  // 256 B aligned segments
+        return at * 4;
+    };
+    const u64 o_roots = seg(c->droots.p, (size_t)(2 + nl) * B * sizeof(Digest));  // [trace, comp, FRI 0..nl-1][B]
+    const u64 o_ood = seg(c->ood.p, (size_t)B * 15 * DE * 8);
+    const u64 o_co = seg(c->coeffs.p, (size_t)B * 15 * DE * 8);
+    const u64 o_dp = seg(c->dp.p, (size_t)B * sizeof(DeepParams));
+    const u64 o_falpha = seg(c->falpha.p, (size_t)nl * B * DE * 8);  // [layer][B][DE]
+    const u64 o_fail = seg(c->dfail.p, (size_t)B * sizeof(int));
+    const u64 o_rem = seg(c->rem.p, (size_t)B * DE * rem_len * 8);
+    const u64 o_dn2 = seg(c->dn2.p, (size_t)B * DE * 8);
+    unsigned char* hx = c->h_xfer.ensure(words * 4);
+    void* hx_dev = nullptr;
+    HIPCHK(hipHostGetDevicePointer(&hx_dev, hx, 0));
+    launch_pack(pk, hx_dev, s);
+    const Digest* roots = (const Digest*)(hx + o_roots);
+    const u64* ood = (const u64*)(hx + o_ood);
+    const u64* co = (const u64*)(hx + o_co);
+    const DeepParams* dps = (const DeepParams*)(hx + o_dp);
+    const Digest* froots = roots + 2 * B;
+    const u64* falpha = (const u64*)(hx + o_falpha);
+    const int* ffail = (const int*)(hx + o_fail);
+    const u64* remh = (const u64*)(hx + o_rem);
+    const u64* dn2h = (const u64*)(hx + o_dn2);
     stage_mark(c, 8);
     ht.mark("launch_rem");
     HIPCHK(hipStreamSynchronize(s));
@@ -904,11 +920,20 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         nent += lay[b].oent.size();
     }
     const size_t nopen = nent * 2 * LB;
-    c->gidx.ensure(allidx.size());
-    c->gval.ensure(nvals);
-    c->gdig.ensure(ndig + 2 * nopen);
     u64* hidx = c->h_idx.ensure(allidx.size());
     memcpy(hidx, allidx.data(), allidx.size() * 8);
+    u64* gv = c->h_gv.ensure(nvals);
+    Digest* gd = c->h_gd.ensure(ndig + 2 * nopen);
+    // the gathers read the indices from, and write the opened values and digests into, the pinned
+    // host blocks directly (device-mapped): no copy-engine transfers whose completion the stream
+    // would wait on (one larger D2H on the SDMA engine cost 17 % of the pipelined throughput, above)
+    void *didx = nullptr, *dgv = nullptr, *dgd = nullptr;
+    HIPCHK(hipHostGetDevicePointer(&didx, hidx, 0));
+    HIPCHK(hipHostGetDevicePointer(&dgv, gv, 0));
+    HIPCHK(hipHostGetDevicePointer(&dgd, gd, 0));
+    const u64* gidx = (const u64*)didx;
+    u64* gval = (u64*)dgv;
+    Digest* gdig = (Digest*)dgd;
     ht.mark("q_idx_host");
     // the gathers (a few hundred microseconds of small kernels) go to the lane's high-priority stream:
     // on its own stream a lane's gathers queued behind the other lanes' chains in the shared hardware
@@ -916,7 +941,6 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     // (sync_rem), so they need no event. Timing mode takes the same stream: stage 9 is measured from
     // the lane stream's last event to an event behind the gathers' copies on this one
     const hipStream_t sq = gather_stream(c);
-    HIPCHK(hipMemcpyAsync(c->gidx.p, hidx, allidx.size() * 8, hipMemcpyHostToDevice, sq));
     ht.mark("q_h2d");
     {
         // the segments lie end to end in allidx: values first, then digests
@@ -924,7 +948,7 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         size_t vo = 0, dof = 0, gbase = 0;  // gbase: index entries consumed by launches already made
         auto add = [&](const void* src, void* dst, bool dig, size_t cnt) {
             if (gs.nseg == GatherSet::MAX) {  // very deep FRI: flush and continue in a new launch
-                launch_gather_set(gs, c->gidx.p + gbase, sq);
+                launch_gather_set(gs, gidx + gbase, sq);
                 gbase += gs.first[gs.nseg];
                 gs = GatherSet{};
             }
@@ -937,25 +961,20 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         const u64* vsrc[2] = {c->lde.p, c->hlde.p};
         for (size_t k = 0; k < vseg.size(); k++) {
             const u64* src = k < 2 ? vsrc[k] : (k == 2 ? c->f0.p : c->flayer[k - 2].p);
-            add(src, c->gval.p + vo, false, vseg[k].second);
+            add(src, gval + vo, false, vseg[k].second);
             vo += vseg[k].second;
         }
         for (size_t k = 0; k < dseg.size(); k++) {
             const Digest* src = k == 0 ? c->tnodes.p : (k == 1 ? c->hnodes.p : c->fnodes[k - 2].p);
-            add(src, c->gdig.p + dof, true, dseg[k].second);
+            add(src, gdig + dof, true, dseg[k].second);
             dof += dseg[k].second;
         }
-        launch_gather_set(gs, c->gidx.p + gbase, sq);
-        const u64* ent = c->gidx.p + nvals + ndig;
-        launch_open_rows(c->lde.p, 7, ent, nent, c->gdig.p + ndig, logn, logbeta, sq);
-        launch_open_rows(c->hlde.p, DE, ent, nent, c->gdig.p + ndig + nopen, logn, logbeta, sq);
+        launch_gather_set(gs, gidx + gbase, sq);
+        const u64* ent = gidx + nvals + ndig;
+        launch_open_rows(c->lde.p, 7, ent, nent, gdig + ndig, logn, logbeta, sq);
+        launch_open_rows(c->hlde.p, DE, ent, nent, gdig + ndig + nopen, logn, logbeta, sq);
     }
     ht.mark("q_launch");
-    u64* gv = c->h_gv.ensure(nvals);
-    Digest* gd = c->h_gd.ensure(ndig + 2 * nopen);
-    if (nvals) HIPCHK(hipMemcpyAsync(gv, c->gval.p, nvals * 8, hipMemcpyDeviceToHost, sq));
-    if (ndig + 2 * nopen)
-        HIPCHK(hipMemcpyAsync(gd, c->gdig.p, (ndig + 2 * nopen) * sizeof(Digest), hipMemcpyDeviceToHost, sq));
     stage_mark(c, 9, sq);
     auto t_q1 = std::chrono::steady_clock::now();
     ht.mark("queries_host");
