@@ -578,9 +578,23 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         c->h_gd.ensure(digs + opens);
     }
 
+    // the unit's small uploads are copied by a kernel from the pinned, device-mapped host blocks: no
+    // copy-engine transfer for the lane stream to wait on (see the replay's pack below). The lane
+    // rewrites these blocks only for its next unit, after this one's stream has drained.
+    auto upload = [&](void* dst, const void* host, size_t bytes) {
+        void* hd = nullptr;
+        HIPCHK(hipHostGetDevicePointer(&hd, const_cast<void*>(host), 0));
+        PackSet u;
+        u.src[0] = hd;
+        u.off[0] = 0;
+        u.words[0] = bytes / 4;
+        u.nseg = 1;
+        launch_pack(u, dst, s);
+    };
+    static_assert(sizeof(AirConst) % 4 == 0 && sizeof(DevCoin) % 4 == 0, "uploads copy 32-bit words");
     AirConst* airs = c->h_air.ensure(B);
     for (int b = 0; b < B; b++) airs[b] = jobs[b].air;
-    HIPCHK(hipMemcpyAsync(c->air.p, airs, B * sizeof(AirConst), hipMemcpyHostToDevice, s));
+    upload(c->air.p, airs, B * sizeof(AirConst));
     // transcript seed: Context::to_elements || public inputs (ProverChannel::new)
     for (auto& j : jobs) {
         u64 e[20];
@@ -602,7 +616,7 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
         }
         c->dcoin.ensure(B);
         c->dfail.ensure(B);
-        HIPCHK(hipMemcpyAsync(c->dcoin.p, hc, B * sizeof(DevCoin), hipMemcpyHostToDevice, s));
+        upload(c->dcoin.p, hc, B * sizeof(DevCoin));
         HIPCHK(hipMemsetAsync(c->dfail.p, 0, B * sizeof(int), s));
     }
 
