@@ -92,7 +92,7 @@ class Exchange:
     On the gloo backend (CPU rehearsal, tests/test_dist.py) the same steps run on host tensors and
     the collectives' Work handles are waited for directly."""
 
-    def __init__(self, rank, world, per, cap, device, dist, send_slots, recv_slots=4, lookahead=4):
+    def __init__(self, rank, world, per, cap, device, dist, send_slots, recv_slots=4, lookahead=4, emulate=0):
         import queue
         import threading
         import torch
@@ -100,6 +100,10 @@ class Exchange:
         self.device, self.dist, self.cuda = device, dist, device.type == "cuda"
         self.hdr = 8 * per
         self.rec = self.hdr + per * cap
+        # records rank 0 receives per step: one per rank, or `emulate` at world size 1 (bench.py
+        # --emulate-ranks: rank 0's record gathered that many times over RCCL, the load of rank 0 at
+        # N = emulate -- the receive buffer, the collectives and the D2H of all records)
+        self.rows = emulate if emulate > 1 and world == 1 and self.cuda else world
         opts = None
         if self.cuda and hasattr(dist, "ProcessGroupNCCL"):
             opts = dist.ProcessGroupNCCL.Options()
@@ -117,8 +121,9 @@ class Exchange:
         self.send_dev = torch.empty(self.rec, dtype=torch.uint8, device=device) if self.cuda else None
         self.next_recv, self.recv_slots = 0, recv_slots
         if rank == 0:
-            self.recv_host = [_pinned(world * self.rec, device).view(world, self.rec) for _ in range(recv_slots)]
-            self.recv_dev = torch.empty((world, self.rec), dtype=torch.uint8, device=device) if self.cuda else None
+            self.recv_host = [_pinned(self.rows * self.rec, device).view(self.rows, self.rec)
+                              for _ in range(recv_slots)]
+            self.recv_dev = torch.empty((self.rows, self.rec), dtype=torch.uint8, device=device) if self.cuda else None
         self.lookahead = max(1, lookahead)
         ring = self.lookahead + 1
         self.in_host = [_pinned(per * REC, device).view(per, REC) for _ in range(ring)]
@@ -214,7 +219,7 @@ class Exchange:
 
     # ---- proofs
     def claim(self):
-        """a free send record for the next batch: (slot, host address, bytes)"""
+        """a free send record for the next batch: (slot, host address, bytes, owning tensor)"""
         s = self.next_send
         if self.send_owned[s]:
             raise RuntimeError("Exchange: more batches in flight than send records")
@@ -222,7 +227,7 @@ class Exchange:
         self._done(self.send_busy[s])
         self.send_busy[s] = None
         self.send_owned[s] = True
-        return s, self.send[s].data_ptr(), self.rec
+        return s, self.send[s].data_ptr(), self.rec, self.send[s]
 
     def gather(self, s):
         """record s holds a complete batch: send it to rank 0 (asynchronous); returns a Gathered,
@@ -236,7 +241,11 @@ class Exchange:
             if self.cuda:
                 self._copy(self.side, self.send_dev, self.send[s])
                 got = list(self.recv_dev.unbind(0)) if self.rank == 0 else None
-                self._coll(self.side, self.dist.gather, self.send_dev, got, dst=0, group=self.group)
+                if self.rows == self.world:
+                    self._coll(self.side, self.dist.gather, self.send_dev, got, dst=0, group=self.group)
+                else:  # emulated ranks (world size 1): one RCCL gather per received record
+                    for q in range(self.rows):
+                        self._coll(self.side, self.dist.gather, self.send_dev, got[q:q + 1], dst=0, group=self.group)
                 if self.rank == 0:
                     self._copy(self.side, self.recv_host[r], self.recv_dev)
             else:
@@ -283,7 +292,7 @@ class Gathered:
             return None
         allb = ex.recv_host[self.slot].numpy()
         out = []
-        for q in range(ex.world):
+        for q in range(ex.rows):
             row = allb[q]
             mv = memoryview(row)
             for i, ln in enumerate(row[:ex.hdr].view(np.int64)):
@@ -302,7 +311,7 @@ def pipelined_steps(submit_fn, collect_fn, batches, depth=2, ex=None, packed=Non
     each step's shard comes from its own scatter, submit_fn(kws, record) proves into an exchange
     record and the completed record is gathered to rank 0; returns the last step's proofs on rank 0,
     None elsewhere, after every exchange of the window has completed."""
-    pending, out = [], None
+    pending, out, failed = [], None, []
     tl = [] if os.environ.get("XFG_BENCH_TIMELINE") else None  # step completion times (stderr)
     ts = []
     # XFG_BENCH_PHASES=1: host time of the loop's phases (scatter, submit, wait, gather), stderr
@@ -318,7 +327,13 @@ def pipelined_steps(submit_fn, collect_fn, batches, depth=2, ex=None, packed=Non
                 p.wait()
             t2 = clk()
         else:
-            p.record_ready()  # the batch is complete in its record (raises on a failed proof)
+            try:
+                p.record_ready()  # the batch is complete in its record (raises on a failed proof)
+            except Exception as e:
+                # the failed proof's length is zeroed in the record, which still travels: every rank
+                # keeps issuing the same collectives (raising here would leave the peers waiting in
+                # this gather until the RCCL timeout); raised once the window's exchanges are done
+                failed.append(e)
             t2 = clk()
             got = ex.gather(s)
         if ph is not None:
@@ -335,8 +350,8 @@ def pipelined_steps(submit_fn, collect_fn, batches, depth=2, ex=None, packed=Non
         s, rec = None, None
         if ex is not None:
             b = ex.inputs(i)
-            s, addr, nbytes = ex.claim()
-            rec = (addr, nbytes)
+            s, addr, nbytes, owner = ex.claim()
+            rec = (addr, nbytes, owner)
         t2 = clk()
         pending.append((submit_fn(b) if rec is None else submit_fn(b, rec), s))
         if ph is not None:
@@ -354,8 +369,12 @@ def pipelined_steps(submit_fn, collect_fn, batches, depth=2, ex=None, packed=Non
             tl.append(clk() - t0)
     if ex is not None:
         t1 = clk()
-        out = out.proofs() if out is not None else None
-        ex.drain()
+        try:
+            out = out.proofs() if out is not None else None
+        finally:
+            ex.drain()
+        if failed:
+            raise failed[0]
         if ph is not None:
             ph["gather"] += clk() - t1
     if tl:
@@ -562,9 +581,42 @@ def verify_rate(prover, proofs, inputs, threads=16, reps=3):
             "host_proofs_per_s": round(len(items) / best["host"], 1), "host_threads": threads}
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(gpus, argv):
+    """`bench.py --gpus N` (N > 1) without a launcher: start N ranks with torch.distributed.run as a
+    CHILD process (this process never touches the GPU, so nothing is exec'd from a GPU-initialised
+    process), relay rank 0's JSON line to stdout and everything else to stderr, and return the child's
+    exit code. Reference harness: src/benchmarks/mod.rs:301-342."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + argv
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1)
+    for line in p.stdout:
+        print(line, end="", file=sys.stdout if line.lstrip().startswith("{") else sys.stderr, flush=True)
+    return p.wait()
+
+
+def check_world(gpus, env):
+    """under a launcher the world size is the launcher's: a --gpus that disagrees is an error, not a
+    silent N = WORLD_SIZE run (the driver's 1 -> 8 curve reads n_gpus from the line)"""
+    world = int(env.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" in env and gpus != world:
+        raise SystemExit(f"bench.py: --gpus {gpus} but the launcher started WORLD_SIZE={world} ranks")
+    return world
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs = ranks; N > 1 without a launcher starts torch.distributed.run itself")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--per-gpu", type=int, default=64)
@@ -579,10 +631,16 @@ def main():
                          "checks the gathered proofs byte for byte against a direct prove_batch")
     ap.add_argument("--dump-proofs", default=None,
                     help="rank 0 writes the last step's gathered proofs here (u32 LE length + bytes each)")
+    ap.add_argument("--emulate-ranks", type=int, default=0,
+                    help="with --dist at world size 1: rank 0's gather receives this many real-size "
+                         "records per step over RCCL (its own, then copies), as rank 0 does at N = this "
+                         "(rehearses the N = 8 exchange load on one GPU)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = check_world(args.gpus, os.environ)
 
     import torch
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -615,11 +673,13 @@ def main():
                   for b in batches]
         # the exchange's pinned records and device buffers (setup): one send record per batch in
         # flight plus the ones whose gathers may still run
-        ex = Exchange(rank, world, per, prover.proof_size_bound(n), device, dist, send_slots=args.depth + 3)
+        ex = Exchange(rank, world, per, prover.proof_size_bound(n), device, dist, send_slots=args.depth + 3,
+                      emulate=args.emulate_ranks)
 
     def submit_fn(kws, record=None):
         if record is not None:  # sharded: proofs written straight into the exchange record
-            return prover.submit_batch_record(kws, n, *record)
+            addr, nbytes, owner = record
+            return prover.submit_batch_record(kws, n, addr, nbytes, owner=owner)
         return prover.submit_batch(kws, trace_length=n)
 
     def collect_fn(pending):
@@ -651,8 +711,12 @@ def main():
     pipe_ms, pipe_sets, pipe_polys = prover.lde_probe(False)
     verified = None
     if rank == 0:
-        assert out is not None and len(out) == per * world
         last = [bytes(x) for x in out]
+        if ex is not None and ex.rows != world:  # emulated ranks: every record received is rank 0's own
+            assert len(last) == ex.rows * per and all(last[q * per:(q + 1) * per] == last[:per]
+                                                      for q in range(ex.rows))
+            last = last[:per]
+        assert len(last) == per * world
         if args.dump_proofs:
             with open(args.dump_proofs, "wb") as f:
                 for p in last:
@@ -722,7 +786,8 @@ def main():
             "gather": "one per step: fixed record of 8 B lengths + proof-size-bound slots per rank",
             "sequencing": "one host worker thread (own process group, high-priority streams), "
                           "collectives in step order; no cross-stream waits on the GPU",
-            "record_bytes_per_rank": ex.rec, "proof_size_bound": ex.cap},
+            "record_bytes_per_rank": ex.rec, "proof_size_bound": ex.cap,
+            "records_received_per_step": ex.rows},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
                      "traffic_source": traffic_src,

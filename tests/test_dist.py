@@ -32,7 +32,7 @@ class _FakeRecordBatch:
     lengths, then one FAKE_CAP slot per proof; `fail` = index of a proof that fails (length 0)"""
 
     def __init__(self, kws, record, fail=None):
-        self.kws, (self.addr, self.nbytes), self.fail = kws, record, fail
+        self.kws, (self.addr, self.nbytes, self.owner), self.fail = kws, record, fail
 
     def record_ready(self):
         proofs = _fake_prove(self.kws)
@@ -42,6 +42,8 @@ class _FakeRecordBatch:
         for i, p in enumerate(proofs):
             hdr[i] = 0 if i == self.fail else len(p)
             C.memmove(self.addr + 8 * k + i * FAKE_CAP, p, len(p))
+        if self.fail is not None:  # as PendingBatch.record_ready: length zeroed, then raise
+            raise RuntimeError(f"proof {self.fail} failed")
 
 
 def _worker(rank, world, port, per, ret, steps=3, depth=2, lookahead=4, fail=None):
@@ -71,14 +73,14 @@ def _worker(rank, world, port, per, ret, steps=3, depth=2, lookahead=4, fail=Non
     try:
         out = bench.pipelined_steps(submit, None, batches, depth, ex, packed)
     except RuntimeError as e:
-        ret.put(("error", str(e)))
+        ret.put((rank, "error", str(e)))
         out = "raised"
     assert seen == [per] * steps
     if rank == 0:
         if out != "raised":
-            ret.put(("ok", [bytes(x) for x in out]))  # rank 0 holds zero-copy views into the ring
+            ret.put((rank, "ok", [bytes(x) for x in out]))  # rank 0 holds zero-copy views into the ring
     else:
-        assert out is None
+        assert out in (None, "raised")
     ex.close()
     dist.barrier()
     dist.destroy_process_group()
@@ -92,18 +94,19 @@ def _free_port():
     return port
 
 
-def _run(world, per, **kw):
+def _run(world, per, expect=1, **kw):
+    """run the ranks; the first `expect` (rank, kind, payload) results, by rank"""
     ctx = mp.get_context("spawn")
     ret = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, per, ret), kwargs=kw) for r in range(world)]
     for p in procs:
         p.start()
-    out = ret.get(timeout=120)
+    out = sorted(ret.get(timeout=120) for _ in range(expect))
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    return out
+    return out[0][1:] if expect == 1 else out
 
 
 @pytest.mark.parametrize("world,per,steps,depth,lookahead", [
@@ -125,9 +128,12 @@ def test_exchange_gloo(world, per, steps, depth, lookahead):
 
 
 def test_exchange_failed_proof_raises_on_rank0():
-    """a proof that failed on another rank (length 0 in its record) must not be read as a proof"""
-    kind, msg = _run(2, 2, steps=2, depth=2, fail=1)
-    assert kind == "error" and "rank 1 proof 1" in msg
+    """a proof that failed on another rank (length 0 in its record) must not be read as a proof on
+    rank 0, and the failing rank raises too -- after the window's collectives, so that no rank is
+    left waiting in a gather (every step here fails on rank 1)"""
+    (r0, k0, m0), (r1, k1, m1) = _run(2, 2, expect=2, steps=3, depth=2, fail=1)
+    assert (r0, k0, r1, k1) == (0, "error", 1, "error")
+    assert "rank 1 proof 1" in m0 and m1 == "proof 1 failed"
 
 
 def test_pack_unpack_roundtrip():
@@ -233,7 +239,7 @@ def test_exchange_device_branch():
     ex.start_inputs(packed, 3)
     for step in range(3):
         assert ex.inputs(step) == kws[:per]  # rank 0's shard of each step
-        s, addr, nbytes = ex.claim()
+        s, addr, nbytes, _ = ex.claim()
         assert nbytes == len(pay)
         k = len(kws[:per])
         mine = _fake_prove(kws[:per])
@@ -315,3 +321,87 @@ def test_config3_eight_ranks_real_prover(tmp_path):
     assert verdicts == [0] * len(got)
     for q, (st, want) in enumerate(firsts):  # the first proof of each rank's shard
         assert st == 0 and got[q * per] == want, q
+
+
+def test_bench_gpus_mismatch_fails_loudly():
+    """under a launcher, --gpus must equal WORLD_SIZE: a mismatch exits non-zero before any GPU work
+    instead of printing a line for a different N"""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "8"], capture_output=True,
+                       text=True, timeout=60, cwd=root, env=env)
+    assert r.returncode != 0 and "--gpus 8 but the launcher started WORLD_SIZE=2" in r.stderr
+
+
+def test_bench_launch_command(monkeypatch):
+    """bench.py --gpus N without WORLD_SIZE starts torch.distributed.run with N ranks on 127.0.0.1 as a
+    child, passes its own arguments through, relays JSON lines to stdout and returns the child's code"""
+    import io
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    seen = {}
+
+    class FakePopen:
+        def __init__(self, cmd, **kw):
+            seen["cmd"] = cmd
+            self.stdout = io.StringIO('torchrun chatter\n{"metric": "m", "n_gpus": 4}\n')
+
+        def wait(self):
+            return 3
+
+    monkeypatch.setattr(subprocess, "Popen", FakePopen)
+    out, err = io.StringIO(), io.StringIO()
+    monkeypatch.setattr(sys, "stdout", out)
+    monkeypatch.setattr(sys, "stderr", err)
+    assert bench.launch_ranks(4, ["--gpus", "4", "--steps", "2"]) == 3
+    cmd = seen["cmd"]
+    assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"] and "--nproc-per-node=4" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "2"] and cmd[-5].endswith("bench.py")
+    assert out.getvalue() == '{"metric": "m", "n_gpus": 4}\n' and "torchrun chatter" in err.getvalue()
+    assert bench.check_world(4, {"WORLD_SIZE": "4"}) == 4 and bench.check_world(1, {}) == 1
+
+
+@pytest.mark.gpu
+def test_bench_gpus_two_without_launcher():
+    """the driver's plain form `bench.py --gpus 2` (no torch.distributed.run in the command) runs two
+    ranks by itself: here sharing the one GPU over gloo, 8 proofs each, all 16 of the last step
+    gathered and GPU-verified on rank 0"""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--per-gpu", "8", "--log-n", "10",
+           "--steps", "2", "--warmup", "1", "--depth", "2", "--no-cpu-baseline", "--no-config5"]
+    env = dict(os.environ, XFG_DIST_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=root, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.strip().splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["verified"] == 16 and line["config"]["proofs_per_step"] == 16
+
+
+@pytest.mark.gpu
+def test_bench_emulated_eight_rank_gather():
+    """rank 0's N = 8 exchange load on one GPU over RCCL (--dist --emulate-ranks 8): eight real-size
+    records received per step, the D2H of all eight, and every received copy equal to the proofs"""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", "1", "--steps", "3", "--warmup", "1", "--per-gpu", "8", "--depth", "2", "--log-n", "10",
+           "--no-cpu-baseline", "--no-config5", "--dist", "--emulate-ranks", "8"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["exchange"]["records_received_per_step"] == 8 and line["verified"] == 8

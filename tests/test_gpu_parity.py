@@ -481,6 +481,92 @@ def test_gpu_batch_verify_matches_host_verifier(prover, ext, n, blowup):
     assert not any(xfgstark.XfgBurnMintVerifier(proof_options=other).batch_verify(items[:3], gpu=prover))
 
 
+def _node_vectors(raw):
+    """BatchMerkleProof node vectors of a paths section: u8 vector count, per vector u8 count + digests"""
+    m, p, vecs = raw[0], 1, []
+    for _ in range(m):
+        c = raw[p]
+        vecs.append([raw[p + 1 + 32 * i:p + 33 + 32 * i] for i in range(c)])
+        p += 1 + 32 * c
+    assert p == len(raw)
+    return vecs
+
+
+def _with_node_vectors(proof, at, vecs):
+    import struct
+    body = bytes([len(vecs)]) + b"".join(bytes([len(v)]) + b"".join(v) for v in vecs)
+    start, ln = at
+    return proof[:start - 4] + struct.pack("<I", len(body)) + body + proof[start + ln:]
+
+
+def _node_vector_mutants(proof):
+    """(mutant, accepted) pairs: openings whose node vectors still parse but do not fit the opening,
+    for the trace, constraint and first FRI layer paths -- a digest moved to the next vector (both
+    directions), one node dropped, two vectors swapped (all rejected) -- and one node appended to a
+    vector, which winter-crypto 0.8's get_root never reads (accepted, as by the oracle's restatement)"""
+    from test_verifier import _sections
+    sec = _sections(proof)
+    out = []
+    for name in ("trace_paths", "constraint_paths", "fri_paths0"):
+        at = sec[name]
+        vecs = _node_vectors(proof[at[0]:at[0] + at[1]])
+        i = next(k for k in range(len(vecs) - 1) if len(vecs[k]) and len(vecs[k + 1]))
+        v = [list(x) for x in vecs]
+        v[i + 1].insert(0, v[i].pop())  # last digest of vector i moved to the front of vector i + 1
+        out.append((_with_node_vectors(proof, at, v), False))
+        v = [list(x) for x in vecs]
+        v[i].append(v[i + 1].pop(0))  # first digest of vector i + 1 moved to the end of vector i
+        out.append((_with_node_vectors(proof, at, v), False))
+        v = [list(x) for x in vecs]
+        v[i].append(v[i][-1])  # one node appended: never read by the walk
+        out.append((_with_node_vectors(proof, at, v), True))
+        v = [list(x) for x in vecs]
+        v[i].insert(0, v[i][-1])  # one node prepended: shifts every node the walk reads
+        out.append((_with_node_vectors(proof, at, v), False))
+        v = [list(x) for x in vecs]
+        v[i].pop()  # one node dropped
+        out.append((_with_node_vectors(proof, at, v), False))
+        if vecs[i] != vecs[i + 1]:
+            v = [list(x) for x in vecs]
+            v[i], v[i + 1] = v[i + 1], v[i]  # two vectors swapped
+            out.append((_with_node_vectors(proof, at, v), False))
+    return out
+
+
+@pytest.mark.parametrize("ext", [1, 2])
+def test_gpu_batch_verify_node_vector_mutants(prover, ext):
+    """vtree_kernel's device walk of the batch openings (node-vector consumption, npairs == nvec,
+    compaction) against the host verifier's BatchMerkleProof::get_root and the oracle verifier on
+    openings whose node vectors parse but do not fit: the GPU, host and oracle verdicts are equal on
+    every item, the misfits are rejected, an appended (unread) node is accepted as winter-crypto
+    0.8's get_root accepts it, and the untouched proofs stay accepted in the same batch"""
+    import xfgstark
+    o = xfgstark.ProofOptions.reference()
+    o.field_extension = ext
+    prover._options = o
+    kws = [synthetic.burn_inputs(2500 + i) for i in range(3)]
+    proofs = [p.to_bytes() for p in prover.prove_batch(kws, trace_length=1024)]
+    airs = [xfgstark.air_consts(**kw) for kw in kws]
+    items, want = [], []
+    for p, a in zip(proofs, airs):
+        items.append((p, a))
+        want.append(True)
+        for m, ok in _node_vector_mutants(p):
+            items.append((m, a))
+            want.append(ok)
+    v = xfgstark.XfgBurnMintVerifier(proof_options=o)
+    host = v.batch_verify(items)
+    dev = v.batch_verify(items, gpu=prover)
+    assert dev == host
+    assert host == want
+    oo = O.options(field_extension=ext)
+    for (p, a), ok in zip(items, host):
+        oa = O.Air()
+        oa.pub = (O.C.c_uint64 * 12)(*a[0])
+        oa.nullifier, oa.commitment = a[1], a[2]
+        assert (O.verify(oa, p, oo) == 0) == ok
+
+
 def test_rejects_options_the_reference_rejects(prover):
     import xfgstark
     kw = synthetic.burn_inputs(3)
@@ -541,6 +627,38 @@ def test_env_knobs_keep_proof_bytes(prover, tmp_path):
         assert got[n] == [hashlib.sha256(b).hexdigest() for b in want], n
     st, oracle = O.prove(oracle_air(synthetic.burn_inputs(700)), 1024, O.options())
     assert st == 0 and hashlib.sha256(oracle).hexdigest() == got[1024][0]
+
+
+_ONE_LANE_CHILD = r"""
+import hashlib, sys
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+import synthetic, xfgstark
+pr = xfgstark.XfgBurnMintProver()
+pend = [pr.submit_batch([synthetic.burn_inputs(1300 + 6 * k + i) for i in range(6)], trace_length=1024)
+        for k in range(2)]
+for p in pend:
+    print(" ".join(hashlib.sha256(r.to_bytes()).hexdigest() for r in p.result()))
+"""
+
+
+def test_one_lane_back_to_back_units_match_oracle():
+    """the per-unit host blocks kernels read and write in place (AIR constants, coins, replay block,
+    opening indices / values / digests: fine-grained pinned memory) are rewritten by the CPU for every
+    unit: ONE lane with 2-proof units proves 12 distinct inputs as 6 units back to back (two batches in
+    flight), and every proof equals the oracle's -- a stale constant, coin or index from the previous
+    unit would change the bytes"""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, XFG_LANES="1", XFG_UNIT="2", XFG_SPLIT_MIN="2")
+    r = subprocess.run([sys.executable, "-c", _ONE_LANE_CHILD, os.path.join(root, "xfg-stark_amd"), root],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = " ".join(r.stdout.split()).split()
+    assert len(got) == 12
+    for i in range(12):
+        st, want = O.prove(oracle_air(synthetic.burn_inputs(1300 + i)), 1024, O.options())
+        assert st == 0 and hashlib.sha256(want).hexdigest() == got[i], i
 
 
 def test_batch_record_and_consumption_rules(prover):

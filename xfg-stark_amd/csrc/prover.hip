@@ -191,8 +191,13 @@ struct DBuf {
     }
 };
 
-// pinned host staging (hipHostMalloc) so D2H/H2D copies are true async DMA, grown with headroom
-template <class T>
+// pinned host staging (hipHostMalloc) so D2H/H2D copies are true async DMA, grown with headroom.
+// Flags: hipHostMallocDefault for DMA staging; MappedHBuf for the blocks kernels read and write in
+// place through hipHostGetDevicePointer (the per-unit AIR constants, coins, replay block, opening
+// indices / values / digests): fine-grained (coherent) memory, so a kernel never reads a line the GPU
+// cached for an earlier unit and its stores reach the host without relying on the dispatch packets'
+// system-scope release (coarse-grained host memory is coherent only at those fences).
+template <class T, unsigned Flags = hipHostMallocDefault>
 struct HBuf {
     T* p = nullptr;
     size_t n = 0;
@@ -203,7 +208,7 @@ struct HBuf {
         p = nullptr;
         n = 0;
         size_t want = cnt + cnt / 4 + 16;
-        HIPCHK(hipHostMalloc((void**)&p, want * sizeof(T), hipHostMallocDefault));
+        HIPCHK(hipHostMalloc((void**)&p, want * sizeof(T), Flags));
         n = want;
         return p;
     }
@@ -215,6 +220,9 @@ struct HBuf {
     T& operator[](size_t i) { return p[i]; }
     T* data() { return p; }
 };
+
+template <class T>
+using MappedHBuf = HBuf<T, hipHostMallocMapped | hipHostMallocCoherent>;
 
 struct TablesHost {
     int LM = -1;
@@ -297,11 +305,11 @@ struct Lane {
     std::vector<DBuf<u64>> flayer;
     std::vector<DBuf<Digest>> fnodes;
     // pinned host staging
-    HBuf<Digest> h_gd;
-    HBuf<u64> h_idx, h_gv;
-    HBuf<unsigned char> h_xfer;  // the replay's inputs, written by launch_pack
-    HBuf<AirConst> h_air;
-    HBuf<DevCoin> h_coin;
+    MappedHBuf<Digest> h_gd;
+    MappedHBuf<u64> h_idx, h_gv;
+    MappedHBuf<unsigned char> h_xfer;  // the replay's inputs, written by launch_pack
+    MappedHBuf<AirConst> h_air;
+    MappedHBuf<DevCoin> h_coin;
     // host scratch of the opening plans and the serialiser, kept across units so steady-state
     // units neither allocate nor page-fault (their cost grew with the shared hosts' load)
     struct {

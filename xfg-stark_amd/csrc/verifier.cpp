@@ -144,8 +144,12 @@ std::string parse_contents(ParsedProof& pf) {
 }
 
 // ------------------------------------------------------------------ batch Merkle root
-// BatchMerkleProof::get_root: the node vectors must hold exactly the siblings the opening plan of
-// `idx` asks for; every node on the way to the root is then recomputed, level by level.
+// BatchMerkleProof::get_root: node vector i must hold at least the siblings the opening plan of
+// `idx` takes from it, in that order; every node on the way to the root is then recomputed, level by
+// level. Nodes past the ones the walk takes are ignored: winter-crypto 0.8's get_root consumes the
+// vectors through per-position pointers and never checks that every node was used (the oracle's
+// batch_root restates the same walk, oracle/orc_stark.c), so an opening with a trailing extra node
+// still verifies there, and here.
 bool merkle_symbolic(const std::vector<u64>& idx, const Paths& paths, u64 L, MerkleSym& out) {
     thread_local BatchOpening plan;
     plan_batch_opening(idx, L, plan);
@@ -168,7 +172,7 @@ bool merkle_symbolic(const std::vector<u64>& idx, const Paths& paths, u64 L, Mer
         lv[0].push_back({L + idx[i], s++});
     }
     for (size_t i = 0; i < plan.size(); i++) {
-        if (paths.cnt[i] != plan.len[i]) return false;
+        if (paths.cnt[i] < plan.len[i]) return false;
         for (unsigned k = 0; k < plan.len[i]; k++) {
             const u64 h = plan.row(i)[k];
             lv[depth - (63 - __builtin_clzll(h))].push_back({h, s});

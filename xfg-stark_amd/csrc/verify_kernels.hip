@@ -64,8 +64,9 @@ __device__ __forceinline__ int block_scan(bool f, int* wsum, int& total) {
 // by leaf index); the distinct leaf pairs take their missing leaf from node vector j (j = the pair's
 // position); then, level by level, the entry at position j of the current sorted list merges with
 // its right neighbour when that is its sibling, else takes its sibling from vector j; the survivors
-// are compacted (block scan) and climb one level. The opening is valid when every vector holds
-// exactly the nodes the walk takes and the root equals the commitment; else flags[proof] |= bit.
+// are compacted (block scan) and climb one level. The opening is valid when every vector holds the
+// nodes the walk takes (nodes past them are ignored, as winter-crypto 0.8's get_root ignores them:
+// verifier.cpp merkle_symbolic) and the root equals the commitment; else flags[proof] |= bit.
 __global__ __launch_bounds__(256) void vtree_kernel(const uint8_t* blob, const VTree* trees, const VTreeLeaf* tleaves,
                                                     const VVec* vecs, uint32_t* flags) {
     __shared__ Digest leaf[512];
@@ -154,7 +155,6 @@ __global__ __launch_bounds__(256) void vtree_kernel(const uint8_t* blob, const V
         nn = total;
         cb ^= 1;
     }
-    if (i < (int)T.nvec && used != vec.cnt) bad = 1;
     __syncthreads();
     if (i == 0) {
         const Digest root = ld_digest(blob + T.root_off);

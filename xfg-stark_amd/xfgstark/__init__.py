@@ -355,10 +355,13 @@ class PendingBatch:
     A batch is consumed once: by result() (which can be called again and returns the same list),
     by packed_into(), or -- for a batch written into a caller's record -- by record_ready()."""
 
-    def __init__(self, prover, ticket, buf, base, cap, outs, lens, sts, record=False):
+    def __init__(self, prover, ticket, buf, base, cap, outs, lens, sts, record=False, owner=None):
         self._p, self._t, self._buf, self._base, self._cap = prover, ticket, buf, base, cap
         self._outs, self._lens, self._sts = outs, lens, sts
         self._record = record  # proofs live in the caller's record: no pooled buffer to release
+        # the object owning the caller's record: kept alive while the workers may still write into
+        # it (until the batch has been waited for, here or in __del__)
+        self._owner = owner
         self._res = None
         self._consumed = None  # name of the call that consumed the batch, if not result()
 
@@ -564,11 +567,13 @@ class XfgBurnMintProver:
             raise self._err(st)
         return PendingBatch(self, ticket.value, buf, base, cap, outs, lens, sts)
 
-    def submit_batch_record(self, inputs, trace_length, addr, nbytes):
+    def submit_batch_record(self, inputs, trace_length, addr, nbytes, owner=None):
         """submit_batch whose output is a caller-owned fixed-size record at host address `addr`
         (record_size bytes): the workers write proof i into slot i and its length into header word
         i, so the record can be handed to a collective (bench.py's exchange step) without packing.
-        The record must stay valid and untouched until PendingBatch.record_ready() returns."""
+        The record must stay untouched until PendingBatch.record_ready() returns; `owner` (the
+        tensor, array or ctypes buffer holding it) is referenced by the PendingBatch so that the
+        memory stays valid at least that long -- without it the caller must keep the record alive."""
         k = len(inputs)
         o = self._options._c()
         cap = _lib.xfg_proof_size_bound(trace_length, C.byref(o))
@@ -591,7 +596,7 @@ class XfgBurnMintProver:
                                          C.byref(ticket))
         if st:
             raise self._err(st)
-        return PendingBatch(self, ticket.value, None, base, cap, outs, lens, sts, record=True)
+        return PendingBatch(self, ticket.value, None, base, cap, outs, lens, sts, record=True, owner=owner)
 
     def _take_buffer(self, size):
         # output buffers are recycled. A new one is an anonymous mapping, not create_string_buffer:
