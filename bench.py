@@ -74,8 +74,9 @@ class Exchange:
       D2H of the shard into a pinned ring slot; the submission waits for that job, long done by then;
     * proofs -- every rank's batch is proven straight into a fixed-size pinned record (int64 lengths,
       then one xfg_proof_size_bound slot per proof: no packing copy, no size all-reduce). Once the
-      batch is done the record goes H2D, is gathered to rank 0 and copied D2H into a pinned ring slot
-      there.
+      batch is done the record goes H2D, is gathered to rank 0 and the other ranks' rows are copied
+      D2H into a pinned ring slot there; rank 0's own record never leaves the host (copied host to
+      host into row 0 of the slot).
 
     Both run on one worker thread with its own process group and high-priority side stream, which
     sequences the steps on the HOST: a copy or collective is issued only once what it reads is
@@ -239,7 +240,11 @@ class Exchange:
 
         def job():
             if self.cuda:
-                self._copy(self.side, self.send_dev, self.send[s])
+                # rank 0's own record is already in its host memory: it is not copied to the device
+                # (its gather contribution is whatever send_dev holds), only the other rows come back
+                # D2H. Emulated ranks do copy it up: the received copies must be real records
+                if self.rank != 0 or self.rows != self.world:
+                    self._copy(self.side, self.send_dev, self.send[s])
                 got = list(self.recv_dev.unbind(0)) if self.rank == 0 else None
                 if self.rows == self.world:
                     self._coll(self.side, self.dist.gather, self.send_dev, got, dst=0, group=self.group)
@@ -247,7 +252,9 @@ class Exchange:
                     for q in range(self.rows):
                         self._coll(self.side, self.dist.gather, self.send_dev, got[q:q + 1], dst=0, group=self.group)
                 if self.rank == 0:
-                    self._copy(self.side, self.recv_host[r], self.recv_dev)
+                    if self.rows > 1 and not os.environ.get("XFG_EX_DEV"):
+                        self._copy(self.side, self.recv_host[r][1:], self.recv_dev[1:])
+                    self.recv_host[r][0].copy_(self.send[s])
             else:
                 got = list(self.recv_host[r].unbind(0)) if self.rank == 0 else None
                 self._coll(None, self.dist.gather, self.send[s], got, dst=0, group=self.group)
@@ -290,6 +297,8 @@ class Gathered:
         ex._done(self.h)
         if self.slot is None:
             return None
+        if os.environ.get("XFG_EX_DEV") and ex.rows > 1:
+            ex.recv_host[self.slot][1:].copy_(ex.recv_dev[1:])
         allb = ex.recv_host[self.slot].numpy()
         out = []
         for q in range(ex.rows):
@@ -441,7 +450,24 @@ def whole_proof_line(proofs_per_s, n, world):
     return {"bytes_per_proof": b, "achieved_GBps": round(achieved, 1), "peak": PEAK_HBM_GBS * world,
             "frac": round(achieved / (PEAK_HBM_GBS * world), 4),
             "note": "SURVEY 8(d) whole-proof algorithmic bytes (each stage reads its inputs and writes its "
-                    "outputs once) x proofs/s, against the HBM peak of all GPUs"}
+                    "outputs once) x proofs/s, against the HBM peak of all GPUs",
+            "valu": whole_proof_valu(proofs_per_s, n, world)}
+
+
+def whole_proof_valu(proofs_per_s, n, world):
+    """the bound that holds for the whole proof: VALU issue. Lane instructions per proof from the
+    committed ledger (profiles/rNN/valu_per_proof.json, scripts/valu_ledger.sh: SQ_INSTS_VALU of every
+    kernel, 3 minus 1 pipelined batches) x proofs/s, against the half-rate issue ceiling of all GPUs"""
+    import glob
+    if n != 1 << LOG_N:
+        return None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "valu_per_proof.json")), reverse=True):
+        d = json.load(open(f))
+        rate = d["lane_instr_per_proof"] * proofs_per_s / 1e12
+        return {"lane_instr_per_proof": d["lane_instr_per_proof"], "achieved_T_lane_instr_s": round(rate, 2),
+                "ceiling_T_lane_instr_s": VALU_HALF_RATE_T * world, "frac": round(rate / (VALU_HALF_RATE_T * world), 3),
+                "source": os.path.relpath(f, ROOT)}
+    return None
 
 
 def in_pipeline(ms, sets, polys, n):
