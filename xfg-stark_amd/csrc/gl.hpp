@@ -136,6 +136,29 @@ __device__ __forceinline__ u64 gl_sub_weak(u64 a, u64 b) {
     const u32 eh = __builtin_subc(dh, 0u, b2, &b3);
     return ((u64)eh << 32) | el;
 }
+// lo - h for a 32-bit h, borrow folded once (+ p): the exact representative in [0, 2^64) for any lo
+// (h <= 2^32 - 1 < p). 5 VALU as one sub / subb chain (the compiler's lowering of gl_sub_weak with a
+// zero high word materialises the first borrow: 6)
+__device__ __forceinline__ u64 gl_sub_u32(u64 lo, u32 h) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    u32 d0, d1, m, e0, e1;
+    u64 bb, bb2;
+    asm("v_sub_co_u32_e64 %[d0], %[bb], %[l0], %[h]\n\t"
+        "s_nop 1\n\t"
+        "v_subb_co_u32_e64 %[d1], %[bb], %[l1], 0, %[bb]\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[m], 0, -1, %[bb]\n\t"
+        "v_sub_co_u32_e64 %[e0], %[bb2], %[d0], %[m]\n\t"
+        "s_nop 1\n\t"
+        "v_subb_co_u32_e64 %[e1], %[bb2], %[d1], 0, %[bb2]"
+        : [d0] "=&v"(d0), [d1] "=&v"(d1), [m] "=&v"(m), [e0] "=&v"(e0), [e1] "=&v"(e1), [bb] "=&s"(bb),
+          [bb2] "=&s"(bb2)
+        : [l0] "v"((u32)lo), [l1] "v"((u32)(lo >> 32)), [h] "v"(h));
+    return ((u64)e1 << 32) | e0;
+#else
+    return gl_sub_weak(lo, h);
+#endif
+}
 // 64x64 -> 128 product as lo + (hi + cv 2^32) 2^64 from four v_mad_u64_u32 (8 VALU):
 // t1 = a0 b1 + (a0 b0 >> 32), t2 = a1 b0 + t1 (carry cv), lo = {lo(a0 b0), lo(t2)}, hi = a1 b1 + hi(t2)
 __device__ __forceinline__ void gl_prod(u64 a, u64 b, u64& lo, u64& hi, u32& cv) {
@@ -162,13 +185,44 @@ __device__ __forceinline__ void gl_prod(u64 a, u64 b, u64& lo, u64& hi, u32& cv)
 
 __host__ __device__ __forceinline__ u64 gl_mul(u64 a, u64 b) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    // a b = lo + hl 2^64 + hh 2^96 == lo + hl EPS - hh; (hh + cv) <= 2^32 - 1 for any a, b < 2^64
-    // (18 VALU; the compiler's own lowering of the same math was 24)
-    u64 lo, hi;
-    u32 cv;
-    gl_prod(a, b, lo, hi, cv);
-    const u32 hh = (u32)(hi >> 32) + cv;
-    return gl_fold(gl_sub_weak(lo, hh), (u32)hi);
+    // a b = lo + hl 2^64 + (hh + c) 2^96 == lo - (hh + c) + hl EPS, (hh + c) <= 2^32 - 1 for any a, b
+    // < 2^64 (15 VALU + 1 SALU; gl_prod + gl_sub_weak + gl_fold was 18, the compiler's own lowering
+    // of the same math 24). The product's carry c is never materialised: it is the borrow-in of the
+    // subtraction lo - hh - c, done on the words of the partial products as they come out of the
+    // mads (lo = (p.lo, t2.lo)), so neither the 64-bit assembly of lo nor hh + c costs an instruction;
+    // a borrow out of the high word adds p (- EPS mod 2^64) once, then gl_fold adds hl EPS.
+    // Each VALU-written carry / borrow mask is read by a VALU only after >= 2 wait states.
+#if defined(XFG_MUL_V1)  // A/B builds only: the round-4 form
+    u64 lo_, hi_;
+    u32 cv_;
+    gl_prod(a, b, lo_, hi_, cv_);
+    return gl_fold(gl_sub_weak(lo_, (u32)(hi_ >> 32) + cv_), (u32)hi_);
+#endif
+    u64 p, t1, t2, hi, x, s, c;
+    const u32 a0 = (u32)a, a1 = (u32)(a >> 32), b0 = (u32)b, b1 = (u32)(b >> 32);
+    asm("v_mad_u64_u32 %[p], %[s], %[a0], %[b0], 0\n\t"
+        "v_lshrrev_b64 %[x], 32, %[p]\n\t"
+        "v_mad_u64_u32 %[t1], %[s], %[a0], %[b1], %[x]\n\t"
+        "v_mad_u64_u32 %[t2], %[c], %[a1], %[b0], %[t1]\n\t"
+        "v_lshrrev_b64 %[x], 32, %[t2]\n\t"
+        "v_mad_u64_u32 %[hi], %[s], %[a1], %[b1], %[x]"
+        : [p] "=&v"(p), [x] "=&v"(x), [t1] "=&v"(t1), [t2] "=&v"(t2), [hi] "=&v"(hi), [s] "=&s"(s), [c] "=&s"(c)
+        : [a0] "v"(a0), [a1] "v"(a1), [b0] "v"(b0), [b1] "v"(b1));
+    u32 d0, d1, m, e0, e1;
+    u64 bb, bb2;
+    asm("s_nop 1\n\t"
+        "v_subb_co_u32_e64 %[d0], %[bb], %[l0], %[hh], %[c]\n\t"
+        "s_nop 1\n\t"
+        "v_subb_co_u32_e64 %[d1], %[bb], %[l1], 0, %[bb]\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[m], 0, -1, %[bb]\n\t"
+        "v_sub_co_u32_e64 %[e0], %[bb2], %[d0], %[m]\n\t"
+        "s_nop 1\n\t"
+        "v_subb_co_u32_e64 %[e1], %[bb2], %[d1], 0, %[bb2]"
+        : [d0] "=&v"(d0), [d1] "=&v"(d1), [m] "=&v"(m), [e0] "=&v"(e0), [e1] "=&v"(e1), [bb] "=&s"(bb),
+          [bb2] "=&s"(bb2)
+        : [l0] "v"((u32)p), [l1] "v"((u32)t2), [hh] "v"((u32)(hi >> 32)), [c] "s"(c));
+    return gl_fold(((u64)e1 << 32) | e0, (u32)hi);
 #else
     return gl_reduce(mulhi64(a, b), a * b);
 #endif

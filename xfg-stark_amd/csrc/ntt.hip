@@ -62,6 +62,32 @@ __device__ __forceinline__ u64 swap_lane_pair(u64 x) {
     const int hi = __builtin_amdgcn_mov_dpp((int)(u32)(x >> 32), 0xB1, 0xF, 0xF, false);
     return (u64)(u32)lo | ((u64)(u32)hi << 32);
 }
+// The same pairing through a buffer resource: output r of the pair's even word sits at byte offset
+// vo + r * step (vo per lane, step wave-uniform), so the part that varies with r rides in the SGPR
+// offset and no 64-bit address is computed per store (the odd lane stores output r + 1: its extra
+// `step` goes into its VGPR offset once)
+typedef u32 u32x4 __attribute__((__vector_size__(16)));
+#ifndef XFG_PAIR_STORES
+#define XFG_PAIR_STORES 1
+#endif
+template <int RR>
+__device__ __forceinline__ void store_pairs_buf(const u64* v, __amdgpu_buffer_rsrc_t rs, u32 vo, u32 step) {
+    if (!XFG_PAIR_STORES) {  // A/B build: one 8-byte store per output, no lane swap
+        const u32 vl = vo + (threadIdx.x & 1) * 8;
+#pragma unroll
+        for (int r = 0; r < RR; r++) buf_st(rs, vl, (u32)r * step, v[r]);
+        return;
+    }
+    const bool odd = threadIdx.x & 1;
+    const u32 vl = vo + (odd ? step : 0u);
+#pragma unroll
+    for (int r = 0; r < RR; r += 2) {
+        const u64 g0 = swap_lane_pair(v[r]), g1 = swap_lane_pair(v[r + 1]);
+        const u64 lo = odd ? g1 : v[r], hi = odd ? v[r + 1] : g0;
+        const u32x4 d = {(u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32)};
+        __builtin_amdgcn_raw_buffer_store_b128(d, rs, (int)vl, (int)((u32)r * step), 0);
+    }
+}
 // at(r): address of output r of the pair's EVEN word (16-byte aligned)
 template <int RR, class AT>
 __device__ __forceinline__ void store_pairs(const u64* v, AT at) {
@@ -124,7 +150,7 @@ __device__ __forceinline__ u64 tw_get(const Tables& T, int k, u64 e, bool inv) {
 // TW2D: the twiddle of element r of a group with k = j % Ns is ltw[r * Ns + k] (a per-step [r][k]
 // table, ntt_pass_a_cos2) instead of w^(r k step) = ltw[r * k * step]
 template <int LOGS, int LOGR, int LOGE, bool INV, bool SEQ_FAST, bool IN_PLACE, int NT, class LD, class ST, class PF,
-          bool TW2D = false>
+          bool TW2D = false, bool CANON_OUT = false>
 __device__ __forceinline__ void stockham(int lognseq, int Ns, const u64* ltw, LD ld, ST st, PF pf) {
     constexpr int S = 1 << LOGS, R = 1 << LOGR, G = S / R, PER = (1 << LOGE) / R;
     const int nseq = 1 << lognseq;
@@ -146,7 +172,7 @@ __device__ __forceinline__ void stockham(int lognseq, int Ns, const u64* ltw, LD
 #pragma unroll
             for (int r = 1; r < R; r++) v[q][r] = gl_mul(v[q][r], TW2D ? ltw[r * Ns + k] : ltw[r * k * step]);
         }
-        dft_reg<LOGR, INV>(v[q]);
+        dft_reg<LOGR, INV, CANON_OUT>(v[q]);
         gs[q] = g0 < groups ? seq : -1;
         gj[q] = j;
     }
@@ -228,7 +254,8 @@ __device__ __forceinline__ void pass_dft(u64* tile, int lognseq, const u64* ltw,
 // steps in 32-bit halves: the low words go through the LDS tile, then the high words through the
 // same tile, so the tile is half the size of a 64-bit one and twice as many blocks fit a CU. Costs
 // twice the LDS instructions and two more barriers per tile.
-template <int LOGS, int LOGE, bool INV, bool FIRST_SEQ_FAST, int NT, class LDG, class STG, class PF, bool TW2D_LAST = false>
+template <int LOGS, int LOGE, bool INV, bool FIRST_SEQ_FAST, int NT, class LDG, class STG, class PF, bool TW2D_LAST = false,
+          bool CANON_OUT = false>
 __device__ __forceinline__ void pass_dft_split(u32* tile, int lognseq, const u64* ltw, LDG ldg, STG stg, PF pf) {
     using PL = Plan<LOGS, LOGE>;
     static_assert(PL::NSTEP == 2 && PL::FIRST_LOGR == LOGE, "two full-radix steps");
@@ -264,7 +291,8 @@ __device__ __forceinline__ void pass_dft_split(u32* tile, int lognseq, const u64
     }
     __syncthreads();
     auto ldl = [&](int sq, int jj, int o) { return (u64)lo[o / G] | ((u64)tile[sq * PITCH + phys2<LOGE>(jj, o)] << 32); };
-    stockham<LOGS, LOGE, LOGE, INV, true, false, NT, decltype(ldl), STG, PF, TW2D_LAST>(lognseq, E, ltw, ldl, stg, pf);
+    stockham<LOGS, LOGE, LOGE, INV, true, false, NT, decltype(ldl), STG, PF, TW2D_LAST, CANON_OUT>(lognseq, E, ltw, ldl, stg,
+                                                                                                 pf);
     __syncthreads();
 }
 
@@ -595,12 +623,15 @@ __global__ __launch_bounds__(256, 3) void ntt_pass_a_r1024(NttArgs a) {
     auto ldg = [&](int seq, int j, int o) -> u64 {
         return gl_mul(buf_ld(rin, (((u32)j << a.logC) + seq) * 8, ((u32)o << a.logC) * 8), pre2[(o >> 5) * TC + seq]);
     };
-    u64* ytile = a.y + (u64)pt * n + ((u64)bx << 13);  // tile-major intermediate: [tile][k1][8]
+    // tile-major intermediate: [tile][k1][8]; table [k1][j2] and intermediate through buffer resources
+    // (per-lane offset in a VGPR, the r * stride part wave-uniform in the SGPR offset)
+    const auto ry = buf_rsrc(a.y + (u64)pt * n + ((u64)bx << 13));
+    const auto rt = buf_rsrc(t4 + col0);
     auto stg = [&](int, int seq, int base, int stride, u64* v) {
-        const u64* tk = t4 + ((u64)base << 10) + col0 + seq;
+        const u32 vt = (((u32)base << 10) + seq) * 8;
 #pragma unroll
-        for (int r = 0; r < RR; r++) v[r] = gl_mul(v[r], tk[(u64)(r * stride) << 10]);
-        store_pairs<RR>(v, [&](int r) { return ytile + ((u64)(base + r * stride) << 3) + (seq & ~1); });
+        for (int r = 0; r < RR; r++) v[r] = gl_mul(v[r], buf_ld(rt, vt, ((u32)(r * stride) << 10) * 8));
+        store_pairs_buf<RR>(v, ry, (((u32)base << 3) + (seq & ~1)) * 8, ((u32)stride << 3) * 8);
     };
     pass_dft_split<LOGR, LOGE, false, true, NT, decltype(ldg), decltype(stg), NoPf, true>(tile, logTC, comb, ldg, stg,
                                                                                        NoPf{});
@@ -624,19 +655,19 @@ __global__ __launch_bounds__(256, 3) void ntt_pass_b_r1024(NttArgs a) {
     for (int i = threadIdx.x; i < C; i += NT) ltw[i] = a.pt[(1 << a.logR) + i];
     // this thread's first-step group (stockham, SEQ_FAST): row seq0 of the tile, columns j0 + 32 r
     const int seq0 = threadIdx.x & (TR - 1), j0 = threadIdx.x >> logTR;
-    const u64* y = a.y + (u64)pt * n + ((u64)(j0 >> 3) << 13) + ((u64)(k10 + seq0) << 3) + (j0 & 7);
+    const auto ry = buf_rsrc(a.y + (u64)pt * n);
+    const u32 vy = ((((u32)(j0 >> 3)) << 13) + ((u32)(k10 + seq0) << 3) + (j0 & 7)) * 8;
     u64 yv[R1];
 #pragma unroll
-    for (int r = 0; r < R1; r++) yv[r] = y[(u64)r << 15];  // column j0 + 32 r: 4 tiles further
+    for (int r = 0; r < R1; r++) yv[r] = buf_ld(ry, vy, ((u32)r << 15) * 8);  // column j0 + 32 r: 4 tiles further
     __syncthreads();
     auto ldg = [&](int, int, int o) -> u64 { return yv[o / G1]; };
-    u64* out = a.out + (u64)pt * n + k10;
-    auto stg = [&](int, int seq, int base, int stride, u64* v) {
-#pragma unroll
-        for (int r = 0; r < RR; r++) v[r] = canon(v[r]);
-        store_pairs<RR>(v, [&](int r) { return out + (seq & ~1) + ((u64)(base + r * stride) << a.logR); });
+    const auto ro = buf_rsrc(a.out + (u64)pt * n + k10);
+    auto stg = [&](int, int seq, int base, int stride, u64* v) {  // the last butterfly level made v canonical
+        store_pairs_buf<RR>(v, ro, ((u32)(seq & ~1) + ((u32)base << a.logR)) * 8, ((u32)stride << a.logR) * 8);
     };
-    pass_dft_split<LOGC, LOGE, false, true, NT>(tile, logTR, ltw, ldg, stg, NoPf{});
+    pass_dft_split<LOGC, LOGE, false, true, NT, decltype(ldg), decltype(stg), NoPf, false, true>(tile, logTR, ltw, ldg, stg,
+                                                                                              NoPf{});
 }
 size_t pass_b_r1024_lds() { return (size_t)((8 * split_pitch(1024, 5, 3) + 1) / 2 + 1024) * sizeof(u64); }
 
@@ -735,8 +766,12 @@ __global__ __launch_bounds__(1 << LOGT) void ntt_pass_b_tq(NttArgs a) {
     const int pt = by, k10 = bx * TR;
     const u64 n = 1ULL << a.logn;
     {
+        // the second step's twiddles as an [r][k] table (w_C^(r k), r, k < 16): each read is a fixed
+        // LDS offset r * 128 from the lane's k * 8, so no per-element address arithmetic (w_C[r k]
+        // needs a multiply and an add per element)
+        static_assert(LOGC == 2 * LOGE, "two full-radix steps");
         const u64* pt4 = a.pt + (1 << a.logR);
-        for (int i = threadIdx.x; i < C; i += NT) ltw[i] = pt4[i];
+        for (int i = threadIdx.x; i < C; i += NT) ltw[i] = pt4[(i >> LOGE) * (i & ((1 << LOGE) - 1))];
     }
     const int seq0 = threadIdx.x / G1, j0 = threadIdx.x % G1;
     const u64 i0 = ((u64)(k10 + seq0) << LOGC) + j0;
@@ -751,12 +786,13 @@ __global__ __launch_bounds__(1 << LOGT) void ntt_pass_b_tq(NttArgs a) {
     __syncthreads();
     auto ldg = [&](int, int, int o) -> u64 { return gl_mul(yv[o / G1], tv[o / G1]); };
     const auto rout = buf_rsrc(a.out + (u64)pt * n + k10);
-    auto stg = [&](int, int seq, int base, int stride, u64* v) {
+    auto stg = [&](int, int seq, int base, int stride, u64* v) {  // the last butterfly level made v canonical
 #pragma unroll
         for (int r = 0; r < RR; r++)
-            buf_st(rout, (seq + ((u32)base << a.logR)) * 8, ((u32)(r * stride) << a.logR) * 8, canon(v[r]));
+            buf_st(rout, (seq + ((u32)base << a.logR)) * 8, ((u32)(r * stride) << a.logR) * 8, v[r]);
     };
-    pass_dft_split<LOGC, LOGE, false, false, NT>(reinterpret_cast<u32*>(tile), logTR, ltw, ldg, stg, NoPf{});
+    pass_dft_split<LOGC, LOGE, false, false, NT, decltype(ldg), decltype(stg), NoPf, true, true>(
+        reinterpret_cast<u32*>(tile), logTR, ltw, ldg, stg, NoPf{});
 }
 
 // ---------------------------------------------------------------- pass B, persistent (forward, no table)
