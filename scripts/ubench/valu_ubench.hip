@@ -66,6 +66,22 @@ DEF(k_cnd_s, "v_cndmask_b32_e64 %0, %0, %1, s[40:41]")
 DEF(k_bfe, "v_bfe_u32 %0, %0, 8, 16")
 DEF64(k_lshr64, "v_lshrrev_b64 %0, 7, %0")
 DEF64(k_mulhi64a, "v_mad_u64_u32 %0, s[40:41], %2, %2, %0")
+// round 5: bitop3 forms (three distinct sources, two-input xor) and three-input xor / or
+DEF(k_bitop3_3, "v_bitop3_b32 %0, %0, %1, %1 bitop3:0x96")
+DEF(k_bitop3_x2, "v_bitop3_b32 %0, %0, %1, 0 bitop3:0x66")
+DEF(k_or3, "v_or3_b32 %0, %0, %1, %0")
+DEF(k_xor_e64, "v_xor_b32_e64 %0, %0, %1")
+DEF(k_alignbit2, "v_alignbit_b32 %0, %0, %1, 16")
+DEF(k_pk_add16, "v_pk_add_u16 %0, %0, %1")
+// VOP2 (e32) against VOP3 (e64) encodings of the same operation
+DEF(k_add_e64, "v_add_u32_e64 %0, %0, %1")
+DEF(k_sub_e64, "v_sub_u32_e64 %0, %0, %1")
+DEF(k_and_e64, "v_and_b32_e64 %0, %0, %1")
+DEF(k_lshr_e64, "v_lshrrev_b32_e64 %0, 7, %0")
+DEF(k_mov_e64, "v_mov_b32_e64 %0, %1")
+DEF(k_subco_e32, "v_sub_co_u32_e32 %0, vcc, %0, %1")
+DEF(k_subco_e64s, "v_sub_co_u32_e64 %0, s[40:41], %0, %1")
+DEF(k_cnd_vcc64, "v_cndmask_b32_e64 %0, %0, %1, vcc")
 
 int main() {
     unsigned* d;
@@ -82,7 +98,12 @@ int main() {
         {"v_addc_co_u32", k_addc}, {"v_cmp_lt_u32", k_cmp32}, {"v_sub_u32", k_sub}, {"v_and_b32", k_and},
         {"v_mul_u32_u24", k_mul24}, {"v_add_co_u32_e64 s", k_addco_s}, {"v_addc_co_u32_e64 s", k_addc_s},
         {"v_lshl_add_u32", k_lshl_add32}, {"v_cndmask_e64 s", k_cnd_s}, {"v_bfe_u32", k_bfe},
-        {"v_lshrrev_b64", k_lshr64}, {"v_mad_u64_u32 s", k_mulhi64a}};
+        {"v_lshrrev_b64", k_lshr64}, {"v_mad_u64_u32 s", k_mulhi64a}, {"v_bitop3 3src", k_bitop3_3},
+        {"v_bitop3 xor2", k_bitop3_x2}, {"v_or3_b32", k_or3}, {"v_xor_b32_e64", k_xor_e64},
+        {"v_alignbit 2src", k_alignbit2}, {"v_pk_add_u16", k_pk_add16}, {"v_add_u32_e64", k_add_e64},
+        {"v_sub_u32_e64", k_sub_e64}, {"v_and_b32_e64", k_and_e64}, {"v_lshrrev_b32_e64", k_lshr_e64},
+        {"v_mov_b32_e64", k_mov_e64}, {"v_sub_co_u32_e32", k_subco_e32}, {"v_sub_co_u32_e64 s", k_subco_e64s},
+        {"v_cndmask_e64 vcc", k_cnd_vcc64}};
     for (auto& k : ks) {
         hipEvent_t a, b;
         hipEventCreate(&a);

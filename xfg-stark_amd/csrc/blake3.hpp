@@ -27,16 +27,48 @@ enum : uint32_t { B3_CHUNK_START = 1, B3_CHUNK_END = 2, B3_PARENT = 4, B3_ROOT =
 
 __host__ __device__ __forceinline__ uint32_t b3_rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
 
-#define XFG_B3_G(a, b, c, d, x, y)            \
-    do {                                      \
-        s[a] = s[a] + s[b] + (x);             \
-        s[d] = b3_rotr(s[d] ^ s[a], 16);      \
-        s[c] = s[c] + s[d];                   \
-        s[b] = b3_rotr(s[b] ^ s[c], 12);      \
-        s[a] = s[a] + s[b] + (y);             \
-        s[d] = b3_rotr(s[d] ^ s[a], 8);       \
-        s[c] = s[c] + s[d];                   \
-        s[b] = b3_rotr(s[b] ^ s[c], 7);       \
+// xor / add of two variables in their VOP3 (e64) encodings: v_xor_b32_e64 issues at 65 T lane-ops/s
+// against 47 for the VOP2 form (profiles/r05/valu_ubench.txt), and BLAKE3 with both its xors and its
+// two-input adds in the e64 encoding ran the leaf kernels 6-10 % faster and the bench 5 % faster
+// (profiles/r05/b3_vop3_ab.txt). Operands the compiler knows are constants keep the plain C form
+// so that it still folds them (the first round's IV words, zero message words).
+__host__ __device__ __forceinline__ uint32_t b3_xor(uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(XFG_B3_VOP2)
+    if (__builtin_constant_p(a) || __builtin_constant_p(b)) return a ^ b;
+    uint32_t r;
+    asm("v_xor_b32_e64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+#else
+    return a ^ b;
+#endif
+}
+__host__ __device__ __forceinline__ uint32_t b3_add(uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(XFG_B3_VOP2)
+    if (__builtin_constant_p(a) || __builtin_constant_p(b)) return a + b;
+    uint32_t r;
+    asm("v_add_u32_e64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+#else
+    return a + b;
+#endif
+}
+
+// a + b + x: v_add3_u32, or the e64 add when the message word is a known zero (padding words)
+__host__ __device__ __forceinline__ uint32_t b3_add3(uint32_t a, uint32_t b, uint32_t x) {
+    if (__builtin_constant_p(x) && x == 0) return b3_add(a, b);
+    return a + b + x;
+}
+
+#define XFG_B3_G(a, b, c, d, x, y)                    \
+    do {                                              \
+        s[a] = b3_add3(s[a], s[b], (x));              \
+        s[d] = b3_rotr(b3_xor(s[d], s[a]), 16);       \
+        s[c] = b3_add(s[c], s[d]);                    \
+        s[b] = b3_rotr(b3_xor(s[b], s[c]), 12);       \
+        s[a] = b3_add3(s[a], s[b], (y));              \
+        s[d] = b3_rotr(b3_xor(s[d], s[a]), 8);        \
+        s[c] = b3_add(s[c], s[d]);                    \
+        s[b] = b3_rotr(b3_xor(s[b], s[c]), 7);        \
     } while (0)
 
 // one round with message words already permuted into m[]
@@ -77,7 +109,7 @@ __host__ __device__ __forceinline__ void b3_compress(const uint32_t cv[8], uint3
     XFG_B3_ROUND(m); XFG_B3_PERMUTE(m);
     XFG_B3_ROUND(m);
 #pragma unroll
-    for (int i = 0; i < 8; i++) out[i] = s[i] ^ s[i + 8];
+    for (int i = 0; i < 8; i++) out[i] = b3_xor(s[i], s[i + 8]);
 }
 
 // BLAKE3 of a single block of `len` (<= 64) bytes given as 16 LE words (zero padded)

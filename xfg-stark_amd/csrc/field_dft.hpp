@@ -33,6 +33,13 @@ __device__ __forceinline__ u64 shr64(u64 x) {
     asm("v_lshrrev_b64 %0, %1, %2" : "=v"(r) : "i"(S), "v"(x));
     return r;
 }
+// 32-bit shift in the e64 encoding (see add_w)
+template <int S>
+__device__ __forceinline__ u32 shr32(u32 x) {
+    u32 r;
+    asm("v_lshrrev_b32_e64 %0, %1, %2" : "=v"(r) : "i"(S), "v"(x));
+    return r;
+}
 // x * 2^S mod p for 0 <= S < 96 (2^96 == -1 is handled by the caller). Canonical result for any
 // u64 x when S > 0; S == 0 returns x as is.
 template <int S>
@@ -41,7 +48,7 @@ __device__ __forceinline__ u64 mul_pow2(u64 x) {
         return x;
     } else if constexpr (S <= 32) {
         // x 2^S = lo + h 2^64 with h = x >> (64 - S) < 2^32 -> lo + h EPS
-        return gl_fold(shl64<S>(x), (u32)(x >> 32) >> (32 - S));
+        return gl_fold(shl64<S>(x), shr32<32 - S>((u32)(x >> 32)));
     } else if constexpr (S < 64) {
         // h = x >> (64 - S) = hh 2^32 + hl -> lo + hl EPS - hh
         const u64 h = shr64<64 - S>(x);
@@ -67,8 +74,9 @@ __host__ __device__ constexpr int brev_c(int x, int bits) {
 // reduce only the subtrahend / addend t (which must be < p for these forms): u + t carries at most
 // once past 2^64 when t < p, and u - t borrows into a value >= EPS when t < p.
 // u + t as s = u + t plus (carry) EPS. The carry out of bit 63 is bit 31 of
-// (a_hi & b_hi) | ((a_hi | b_hi) & ~s_hi): one full-rate v_bitop3_b32 (truth table 0xd4 over
-// src0, src1, src2 = a_hi, b_hi, s_hi) and one full-rate shift, then one v_mad_u64_u32 adds
+// (a_hi & b_hi) | ((a_hi | b_hi) & ~s_hi): one v_bitop3_b32 (truth table 0xd4 over src0, src1,
+// src2 = a_hi, b_hi, s_hi) and one shift in its e64 encoding (70 T lane-ops/s against 48 for the
+// VOP2 form, profiles/r05/valu_ubench.txt), then one v_mad_u64_u32 adds
 // carry * EPS -- 2 half-rate + 2 full-rate instructions and no VALU -> SGPR -> VALU mask hand-off
 // (the compare / cndmask form was 4 half-rate instructions plus an s_nop). No second carry: with
 // t < p, s = u + t - 2^64 <= p - 2 and s + EPS < 2^64.
@@ -77,7 +85,7 @@ __device__ __forceinline__ u64 add_w(u64 a, u64 b) {  // b < p
     u32 c;
     asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(s) : "v"(a), "v"(b));
     asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xd4\n\t"
-        "v_lshrrev_b32 %0, 31, %0"
+        "v_lshrrev_b32_e64 %0, 31, %0"
         : "=&v"(c)
         : "v"((u32)(a >> 32)), "v"((u32)(b >> 32)), "v"((u32)(s >> 32)));
     return s + (u64)c * EPS;
