@@ -75,8 +75,8 @@ class Exchange:
     * proofs -- every rank's batch is proven straight into a fixed-size pinned record (int64 lengths,
       then one xfg_proof_size_bound slot per proof: no packing copy, no size all-reduce). Once the
       batch is done the record goes H2D, is gathered to rank 0 and the other ranks' rows are copied
-      D2H into a pinned ring slot there; rank 0's own record never leaves the host (copied host to
-      host into row 0 of the slot).
+      D2H into a pinned ring slot there; rank 0's own record never leaves the host (its proofs are
+      read from the send record).
 
     Both run on one worker thread with its own process group and high-priority side stream, which
     sequences the steps on the HOST: a copy or collective is issued only once what it reads is
@@ -102,8 +102,9 @@ class Exchange:
         self.hdr = 8 * per
         self.rec = self.hdr + per * cap
         # records rank 0 receives per step: one per rank, or `emulate` at world size 1 (bench.py
-        # --emulate-ranks: rank 0's record gathered that many times over RCCL, the load of rank 0 at
-        # N = emulate -- the receive buffer, the collectives and the D2H of all records)
+        # --emulate-ranks K: the load of rank 0 at N = K -- one RCCL gather per step that receives K
+        # real-size records, and the D2H of the K - 1 "peer" rows; those rows are copies of the first
+        # record this rank sent, standing in for the peers' proofs)
         self.rows = emulate if emulate > 1 and world == 1 and self.cuda else world
         opts = None
         if self.cuda and hasattr(dist, "ProcessGroupNCCL"):
@@ -118,8 +119,11 @@ class Exchange:
         self.send_busy = [None] * send_slots  # the gather job that last read the slot
         self.send_owned = [False] * send_slots  # claimed by a batch that has not been gathered yet
         self.next_send = 0
-        # one device record each way: the gather worker runs one gather at a time
-        self.send_dev = torch.empty(self.rec, dtype=torch.uint8, device=device) if self.cuda else None
+        # one device record each way (emulated: the K-row contribution): the gather worker runs one
+        # gather at a time
+        self.send_dev = torch.empty(self.rec * (self.rows // world), dtype=torch.uint8, device=device) \
+            if self.cuda else None
+        self.peer_rows_set = False
         self.next_recv, self.recv_slots = 0, recv_slots
         if rank == 0:
             self.recv_host = [_pinned(self.rows * self.rec, device).view(self.rows, self.rec)
@@ -239,29 +243,32 @@ class Exchange:
             self.next_recv = (r + 1) % self.recv_slots
 
         def job():
+            import torch
             if self.cuda:
                 # rank 0's own record is already in its host memory: it is not copied to the device
-                # (its gather contribution is whatever send_dev holds), only the other rows come back
-                # D2H. Emulated ranks do copy it up: the received copies must be real records
-                if self.rank != 0 or self.rows != self.world:
-                    self._copy(self.side, self.send_dev, self.send[s])
-                got = list(self.recv_dev.unbind(0)) if self.rank == 0 else None
-                if self.rows == self.world:
-                    self._coll(self.side, self.dist.gather, self.send_dev, got, dst=0, group=self.group)
-                else:  # emulated ranks (world size 1): one RCCL gather per received record
-                    for q in range(self.rows):
-                        self._coll(self.side, self.dist.gather, self.send_dev, got[q:q + 1], dst=0, group=self.group)
-                if self.rank == 0:
-                    if self.rows > 1 and not os.environ.get("XFG_EX_DEV"):
-                        self._copy(self.side, self.recv_host[r][1:], self.recv_dev[1:])
-                    self.recv_host[r][0].copy_(self.send[s])
+                # (its gather contribution is whatever send_dev holds) nor back, Gathered.proofs reads
+                # it from the send record; only the other rows come back D2H. Emulated ranks do copy
+                # it up: the rows standing in for the peers are copies of it
+                emul = self.rows != self.world
+                if self.rank != 0 or emul:
+                    self._copy(self.side, self.send_dev[:self.rec], self.send[s])
+                if emul and not self.peer_rows_set:  # once: the peer rows' content (device copies)
+                    with torch.cuda.stream(self.side):
+                        self.send_dev.view(self.rows, self.rec)[1:].copy_(
+                            self.send_dev[:self.rec].expand(self.rows - 1, self.rec))
+                    self.side.synchronize()
+                    self.peer_rows_set = True
+                got = [self.recv_dev.view(-1)] if emul else (list(self.recv_dev.unbind(0)) if self.rank == 0 else None)
+                self._coll(self.side, self.dist.gather, self.send_dev, got, dst=0, group=self.group)
+                if self.rank == 0 and self.rows > 1:
+                    self._copy(self.side, self.recv_host[r][1:], self.recv_dev[1:])
             else:
                 got = list(self.recv_host[r].unbind(0)) if self.rank == 0 else None
                 self._coll(None, self.dist.gather, self.send[s], got, dst=0, group=self.group)
         h = self._submit(job)
         self.send_busy[s] = h
         self.send_owned[s] = False
-        return Gathered(self, h, r)
+        return Gathered(self, h, r, s)
 
     def drain(self):
         for h in self.send_busy + [p[1] for p in self.in_pending if p]:
@@ -285,24 +292,24 @@ class _Job:
 class Gathered:
     """one step's gathered proofs on rank 0 (a handle on the asynchronous exchange)"""
 
-    def __init__(self, ex, h, slot):
-        self.ex, self.h, self.slot = ex, h, slot
+    def __init__(self, ex, h, slot, send_slot):
+        self.ex, self.h, self.slot, self.send_slot = ex, h, slot, send_slot
 
     def proofs(self):
         """waits for the exchange; rank 0: all ranks' proofs in rank order, zero-copy memoryviews
-        into the pinned ring slot (valid until the slot is reused, recv_slots gathers later); None
-        elsewhere. A zero or oversized length (a failed proof) raises."""
+        into the pinned ring slot and, for rank 0's own proofs, into its send record (valid until the
+        slot is reused, recv_slots gathers later, and the record is claimed again, send_slots batches
+        later); None elsewhere. A zero or oversized length (a failed proof) raises."""
         import numpy as np
         ex = self.ex
         ex._done(self.h)
         if self.slot is None:
             return None
-        if os.environ.get("XFG_EX_DEV") and ex.rows > 1:
-            ex.recv_host[self.slot][1:].copy_(ex.recv_dev[1:])
         allb = ex.recv_host[self.slot].numpy()
         out = []
         for q in range(ex.rows):
-            row = allb[q]
+            # rank 0's own record never left its host memory (CUDA path): read it from the send record
+            row = ex.send[self.send_slot].numpy() if q == 0 and ex.cuda else allb[q]
             mv = memoryview(row)
             for i, ln in enumerate(row[:ex.hdr].view(np.int64)):
                 if not 0 < ln <= ex.cap:
@@ -738,9 +745,9 @@ def main():
     verified = None
     if rank == 0:
         last = [bytes(x) for x in out]
-        if ex is not None and ex.rows != world:  # emulated ranks: every record received is rank 0's own
-            assert len(last) == ex.rows * per and all(last[q * per:(q + 1) * per] == last[:per]
-                                                      for q in range(ex.rows))
+        if ex is not None and ex.rows != world:  # emulated ranks: the stand-in peer rows
+            peer = last[per:2 * per]
+            assert len(last) == ex.rows * per and all(last[q * per:(q + 1) * per] == peer for q in range(1, ex.rows))
             last = last[:per]
         assert len(last) == per * world
         if args.dump_proofs:

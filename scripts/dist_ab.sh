@@ -1,9 +1,9 @@
 #!/bin/bash
 # GPU box: bench.py at world size 1 without and with the RCCL exchange step (--dist under
 # torch.distributed.run: one scatter of packed inputs per step, gather of fixed-size proof records),
-# and with rank 0's N = EMUL exchange load (--dist --emulate-ranks EMUL, default 8: EMUL records
-# received over RCCL and copied D2H per step), REPS interleaved rounds. XFG_BENCH_PHASES splits the
-# --dist loops' host time (scatter / submit / wait / gather).
+# and with rank 0's N = EMUL exchange load (--dist --emulate-ranks EMUL, default 8: one RCCL gather
+# per step receiving EMUL real-size records, the EMUL - 1 peer rows copied D2H), REPS interleaved
+# rounds. XFG_BENCH_PHASES splits the --dist loops' host time (scatter / submit / wait / gather).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out/dist
