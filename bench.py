@@ -471,9 +471,11 @@ def whole_proof_valu(proofs_per_s, n, world):
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "valu_per_proof.json")), reverse=True):
         d = json.load(open(f))
         rate = d["lane_instr_per_proof"] * proofs_per_s / 1e12
+        # the ceiling of the proof's instruction mix (scripts/valu_ceiling.py: measured issue rate per
+        # instruction form over each kernel's ISA, weighted by its share), else the half-rate class
+        ceil = d.get("ceiling_T_lane_instr_s", VALU_HALF_RATE_T) * world
         return {"lane_instr_per_proof": d["lane_instr_per_proof"], "achieved_T_lane_instr_s": round(rate, 2),
-                "ceiling_T_lane_instr_s": VALU_HALF_RATE_T * world, "frac": round(rate / (VALU_HALF_RATE_T * world), 3),
-                "source": os.path.relpath(f, ROOT)}
+                "ceiling_T_lane_instr_s": ceil, "frac": round(rate / ceil, 3), "source": os.path.relpath(f, ROOT)}
     return None
 
 
@@ -497,7 +499,8 @@ def pmc_record(per, n, blowup):
     return None, None
 
 
-VALU_HALF_RATE_T = 36.0  # measured issue ceiling of the 64-bit / carry VALU forms (scripts/ubench/valu_ubench.hip)
+VALU_HALF_RATE_T = 36.0  # measured issue rate of the 64-bit / carry / three-source VALU forms the field code is
+#                          made of (profiles/r05/valu_ubench.txt; the LDE passes' mix ceiling is 37.0)
 
 
 def valu_roofline(rec, lde_ms, outputs):
