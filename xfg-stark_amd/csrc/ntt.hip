@@ -787,6 +787,7 @@ __global__ __launch_bounds__(1 << LOGT) void ntt_pass_b_tq(NttArgs a) {
     auto ldg = [&](int, int, int o) -> u64 { return gl_mul(yv[o / G1], tv[o / G1]); };
     const auto rout = buf_rsrc(a.out + (u64)pt * n + k10);
     auto stg = [&](int, int seq, int base, int stride, u64* v) {  // the last butterfly level made v canonical
+        // (16-byte paired stores, store_pairs_buf, measured neutral here: profiles/r05/tqp_ab.txt)
 #pragma unroll
         for (int r = 0; r < RR; r++)
             buf_st(rout, (seq + ((u32)base << a.logR)) * 8, ((u32)(r * stride) << a.logR) * 8, v[r]);
