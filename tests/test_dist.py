@@ -405,3 +405,22 @@ def test_bench_emulated_eight_rank_gather():
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["exchange"]["records_received_per_step"] == 8 and line["verified"] == 8
+
+
+def test_bench_roofline_records():
+    """bench.py's roofline fields read the newest committed records: the trace-LDE PMC record of the
+    64-proof 2^16 launch set (traffic, lane instructions per output) and the whole-proof VALU ledger
+    with its instruction-mix ceiling; SURVEY 8(d)'s per-proof algorithmic bytes at configs[2]"""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    assert bench.whole_proof_bytes(1 << 16, 8) == 221_246_464
+    rec, src = bench.pmc_record(64, 1 << 16, 8)
+    assert rec and src.startswith("profiles/r") and rec["traffic_bytes"] > rec["algorithmic_bytes"]
+    v = bench.valu_roofline(rec, 1.4, 7 * 64 * (1 << 16) * 8)
+    assert 150 < v["lane_instr_per_output"] < 200 and 0 < v["frac"] < 1.2
+    w = bench.whole_proof_valu(14000.0, 1 << 16, 1)
+    assert w and w["ceiling_T_lane_instr_s"] > 36 and 0 < w["frac"] < 1 and w["source"].endswith("valu_per_proof.json")
+    assert bench.whole_proof_valu(14000.0, 1 << 20, 1) is None  # the ledger is for configs[2] only
+    assert bench.whole_proof_valu(28000.0, 1 << 16, 2)["ceiling_T_lane_instr_s"] == 2 * w["ceiling_T_lane_instr_s"]
