@@ -84,35 +84,6 @@ __host__ __device__ __forceinline__ uint32_t b3_add3(uint32_t a, uint32_t b, uin
         XFG_B3_G(3, 4, 9, 14, m[14], m[15]);              \
     } while (0)
 
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(XFG_B3_VOP2) && !defined(XFG_B3_COMPILER_SCHED)
-// The device rounds issue in a fixed order: each half-round (four independent G functions, 48 VALU)
-// is one asm block generated by scripts/b3_sched_gen.py -- fast and slow instructions of different
-// G's alternating, an s_nop after each fast one. gfx950 issues its two-source e64 xor / add about
-// 1.7x faster than add3 / alignbit, and how close a mix of the two gets to its harmonic rate depends
-// on the order: the compiler's order of the same 680 instructions per compression issues at 35-37 T
-// lane-instructions/s, fixed orders at 40-42 without s_nops and 42-45 with them
-// (profiles/r05/b3_sched.txt). Round 1 stays in C so that the compiler folds the IV / counter /
-// flag constants of the state. No operand can alias another: from round 2 on every state word is
-// an output of the previous block, and the message words are read-only.
-#include "b3_sched.inc"
-#define XFG_B3_ROUND(m)                                                                             \
-    do {                                                                                            \
-        asm(XFG_B3_HALF_ASM                                                                         \
-            : "+v"(s[0]), "+v"(s[4]), "+v"(s[8]), "+v"(s[12]), "+v"(s[1]), "+v"(s[5]), "+v"(s[9]),   \
-              "+v"(s[13]), "+v"(s[2]), "+v"(s[6]), "+v"(s[10]), "+v"(s[14]), "+v"(s[3]), "+v"(s[7]), \
-              "+v"(s[11]), "+v"(s[15])                                                              \
-            : "v"(m[0]), "v"(m[1]), "v"(m[2]), "v"(m[3]), "v"(m[4]), "v"(m[5]), "v"(m[6]), "v"(m[7])); \
-        asm(XFG_B3_HALF_ASM                                                                         \
-            : "+v"(s[0]), "+v"(s[5]), "+v"(s[10]), "+v"(s[15]), "+v"(s[1]), "+v"(s[6]), "+v"(s[11]), \
-              "+v"(s[12]), "+v"(s[2]), "+v"(s[7]), "+v"(s[8]), "+v"(s[13]), "+v"(s[3]), "+v"(s[4]),  \
-              "+v"(s[9]), "+v"(s[14])                                                               \
-            : "v"(m[8]), "v"(m[9]), "v"(m[10]), "v"(m[11]), "v"(m[12]), "v"(m[13]), "v"(m[14]),     \
-              "v"(m[15]));                                                                          \
-    } while (0)
-#else
-#define XFG_B3_ROUND(m) XFG_B3_ROUND_C(m)
-#endif
-
 // BLAKE3 message permutation applied in registers between rounds (compile-time indices)
 #define XFG_B3_PERMUTE(m)                                                                   \
     do {                                                                                    \
@@ -124,29 +95,67 @@ __host__ __device__ __forceinline__ uint32_t b3_add3(uint32_t a, uint32_t b, uin
         m[14] = t15; m[15] = t8;                                                            \
     } while (0)
 
-// compression returning the first 8 output words (chaining value / digest)
+// the same permutation as a constexpr map on zero masks: round r + 1 reads m'[i] = m[P[i]]
+__host__ __device__ constexpr unsigned b3_perm_mask(unsigned z) {
+    constexpr int P[16] = {2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8};
+    unsigned r = 0;
+    for (int i = 0; i < 16; i++) r |= ((z >> P[i]) & 1u) << i;
+    return r;
+}
+
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(XFG_B3_VOP2) && !defined(XFG_B3_COMPILER_SCHED)
+// The device rounds 2-7 issue in a fixed order: each half-round (four independent G functions, 48
+// VALU) is one asm block generated by scripts/b3_sched_gen.py -- fast and slow instructions of
+// different G's alternating, an s_nop after each fast one. gfx950 issues its two-source e64 xor / add
+// about 1.7x faster than add3 / alignbit, and how close a mix of the two gets to its harmonic rate
+// depends on the order: the compiler's order of the same 680 instructions per compression issues at
+// 35-37 T lane-instructions/s, fixed orders at 40-42 without s_nops and 42-45 with them
+// (profiles/r05/b3_sched.txt). Message words known to be zero (the padding of short element hashes,
+// tracked through the permutation as the mask Z) select a block whose add3 for that word is a fast
+// two-source add. Round 1 stays in C so that the compiler folds the IV / counter / flag constants of
+// the state. No operand can alias another: from round 2 on every state word is an output of the
+// previous block, and the message words are read-only.
+#include "b3_sched.inc"
+#define XFG_B3_ROUND_Z(m, Z)                                                                         \
+    do {                                                                                             \
+        b3_half<(Z) & 0xFFu>(s[0], s[4], s[8], s[12], s[1], s[5], s[9], s[13], s[2], s[6], s[10], s[14],  \
+                             s[3], s[7], s[11], s[15], m[0], m[1], m[2], m[3], m[4], m[5], m[6], m[7]);   \
+        b3_half<((Z) >> 8) & 0xFFu>(s[0], s[5], s[10], s[15], s[1], s[6], s[11], s[12], s[2], s[7], s[8], \
+                                    s[13], s[3], s[4], s[9], s[14], m[8], m[9], m[10], m[11], m[12], m[13], \
+                                    m[14], m[15]);                                                   \
+    } while (0)
+#else
+#define XFG_B3_ROUND_Z(m, Z) XFG_B3_ROUND_C(m)
+#endif
+
+// compression returning the first 8 output words (chaining value / digest); ZM: message words known
+// to be zero (bit i = m[i]), a compile-time hint for the device rounds (any value is correct for 0)
+template <unsigned ZM = 0>
 __host__ __device__ __forceinline__ void b3_compress(const uint32_t cv[8], uint32_t m[16], uint32_t block_len,
                                                      uint64_t counter, uint32_t flags, uint32_t out[8]) {
     uint32_t s[16] = {cv[0], cv[1], cv[2], cv[3], cv[4], cv[5], cv[6], cv[7],
                       XFG_B3_IV0, XFG_B3_IV1, XFG_B3_IV2, XFG_B3_IV3,
                       (uint32_t)counter, (uint32_t)(counter >> 32), block_len, flags};
+    constexpr unsigned Z2 = b3_perm_mask(ZM), Z3 = b3_perm_mask(Z2), Z4 = b3_perm_mask(Z3),
+                       Z5 = b3_perm_mask(Z4), Z6 = b3_perm_mask(Z5), Z7 = b3_perm_mask(Z6);
     XFG_B3_ROUND_C(m); XFG_B3_PERMUTE(m);
-    XFG_B3_ROUND(m); XFG_B3_PERMUTE(m);
-    XFG_B3_ROUND(m); XFG_B3_PERMUTE(m);
-    XFG_B3_ROUND(m); XFG_B3_PERMUTE(m);
-    XFG_B3_ROUND(m); XFG_B3_PERMUTE(m);
-    XFG_B3_ROUND(m); XFG_B3_PERMUTE(m);
-    XFG_B3_ROUND(m);
+    XFG_B3_ROUND_Z(m, Z2); XFG_B3_PERMUTE(m);
+    XFG_B3_ROUND_Z(m, Z3); XFG_B3_PERMUTE(m);
+    XFG_B3_ROUND_Z(m, Z4); XFG_B3_PERMUTE(m);
+    XFG_B3_ROUND_Z(m, Z5); XFG_B3_PERMUTE(m);
+    XFG_B3_ROUND_Z(m, Z6); XFG_B3_PERMUTE(m);
+    XFG_B3_ROUND_Z(m, Z7);
 #pragma unroll
     for (int i = 0; i < 8; i++) out[i] = b3_xor(s[i], s[i + 8]);
 }
 
 // BLAKE3 of a single block of `len` (<= 64) bytes given as 16 LE words (zero padded)
+template <unsigned ZM = 0>
 __host__ __device__ __forceinline__ Digest b3_hash_block(uint32_t m[16], uint32_t len) {
     const uint32_t iv[8] = {XFG_B3_IV0, XFG_B3_IV1, XFG_B3_IV2, XFG_B3_IV3,
                             XFG_B3_IV4, XFG_B3_IV5, XFG_B3_IV6, XFG_B3_IV7};
     Digest d;
-    b3_compress(iv, m, len, 0, B3_CHUNK_START | B3_CHUNK_END | B3_ROOT, d.w);
+    b3_compress<ZM>(iv, m, len, 0, B3_CHUNK_START | B3_CHUNK_END | B3_ROOT, d.w);
     return d;
 }
 // Blake3_256::merge([a, b]) = BLAKE3(a || b)
@@ -169,7 +178,7 @@ __host__ __device__ __forceinline__ Digest b3_hash_elems(const uint64_t* e) {
         m[2 * i + 1] = (uint32_t)(v >> 32);
     }
     if constexpr (K <= 8) {
-        return b3_hash_block(m, 8 * K);
+        return b3_hash_block<0xFFFFu & ~((1u << (2 * K)) - 1u)>(m, 8 * K);  // words 2K.. are zero
     } else {
         const uint32_t iv[8] = {XFG_B3_IV0, XFG_B3_IV1, XFG_B3_IV2, XFG_B3_IV3,
                                 XFG_B3_IV4, XFG_B3_IV5, XFG_B3_IV6, XFG_B3_IV7};
@@ -182,7 +191,7 @@ __host__ __device__ __forceinline__ Digest b3_hash_elems(const uint64_t* e) {
             m[2 * i + 1] = (uint32_t)(v >> 32);
         }
         Digest d;
-        b3_compress(cv, m, 8 * (K - 8), 0, B3_CHUNK_END | B3_ROOT, d.w);
+        b3_compress<0xFFFFu & ~((1u << (2 * (K - 8))) - 1u)>(cv, m, 8 * (K - 8), 0, B3_CHUNK_END | B3_ROOT, d.w);
         return d;
     }
 }

@@ -43,7 +43,7 @@ __device__ __forceinline__ Digest dev_merge_int(const Digest& seed, u64 v) {
     m[9] = (uint32_t)(v >> 32);
 #pragma unroll
     for (int i = 10; i < 16; i++) m[i] = 0;
-    return b3_hash_block(m, 40);
+    return b3_hash_block<0xFC00u>(m, 40);  // words 10..15 are zero
 }
 // acceptance of a drawn candidate (counter, first two LE words): every element < p
 struct AcceptP {
