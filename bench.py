@@ -740,6 +740,8 @@ def main():
                           packed[args.warmup:] if packed else None)
     barrier()
     el = time.perf_counter() - t0
+    if os.environ.get("XFG_BENCH_TIMELINE"):  # the window in the profiler's clock (CLOCK_MONOTONIC ns)
+        print(f"window ns: {int(t0 * 1e9)} {int((t0 + el) * 1e9)}", file=sys.stderr)
     el_t = torch.tensor([el], dtype=torch.float64, device=device)
     if dist is not None:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
