@@ -1,6 +1,6 @@
 #!/bin/bash
-# GPU box (round 5): BLAKE3 half-rounds specialised on known-zero message words (the add3 of a zero
-# padding word as a two-source e64 add) -- the -m gpu suite on the tree's build, then bench proofs/s
+# GPU box (round 5): a BLAKE3 schedule change (first: half-rounds specialised on known-zero message words, the add3 of a zero
+# padding word as a two-source e64 add; then round 1's diagonal half as a block) -- the -m gpu suite on the tree's build, then bench proofs/s
 # against the previous commit (head) and the compiler-scheduled rounds (cs)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"

@@ -71,17 +71,26 @@ __host__ __device__ __forceinline__ uint32_t b3_add3(uint32_t a, uint32_t b, uin
         s[b] = b3_rotr(b3_xor(s[b], s[c]), 7);        \
     } while (0)
 
-// one round with message words already permuted into m[] (compiler-scheduled)
-#define XFG_B3_ROUND_C(m)                                 \
+// one round with message words already permuted into m[] (compiler-scheduled): column half, then
+// diagonal half
+#define XFG_B3_COL_C(m)                                   \
     do {                                                  \
         XFG_B3_G(0, 4, 8, 12, m[0], m[1]);                \
         XFG_B3_G(1, 5, 9, 13, m[2], m[3]);                \
         XFG_B3_G(2, 6, 10, 14, m[4], m[5]);               \
         XFG_B3_G(3, 7, 11, 15, m[6], m[7]);               \
+    } while (0)
+#define XFG_B3_DIAG_C(m)                                  \
+    do {                                                  \
         XFG_B3_G(0, 5, 10, 15, m[8], m[9]);               \
         XFG_B3_G(1, 6, 11, 12, m[10], m[11]);             \
         XFG_B3_G(2, 7, 8, 13, m[12], m[13]);              \
         XFG_B3_G(3, 4, 9, 14, m[14], m[15]);              \
+    } while (0)
+#define XFG_B3_ROUND_C(m) \
+    do {                  \
+        XFG_B3_COL_C(m);  \
+        XFG_B3_DIAG_C(m); \
     } while (0)
 
 // BLAKE3 message permutation applied in registers between rounds (compile-time indices)
@@ -112,19 +121,20 @@ __host__ __device__ constexpr unsigned b3_perm_mask(unsigned z) {
 // 35-37 T lane-instructions/s, fixed orders at 40-42 without s_nops and 42-45 with them
 // (profiles/r05/b3_sched.txt). Message words known to be zero (the padding of short element hashes,
 // tracked through the permutation as the mask Z) select a block whose add3 for that word is a fast
-// two-source add. Round 1 stays in C so that the compiler folds the IV / counter / flag constants of
-// the state. No operand can alias another: from round 2 on every state word is an output of the
-// previous block, and the message words are read-only.
+// two-source add. No operand can alias another: every state word a block reads is an output of the
+// C column half or of the previous block, and the message words are read-only.
 #include "b3_sched.inc"
+#define XFG_B3_DIAG_Z(m, Z)                                                                          \
+    b3_half<((Z) >> 8) & 0xFFu>(s[0], s[5], s[10], s[15], s[1], s[6], s[11], s[12], s[2], s[7], s[8], s[13], \
+                                s[3], s[4], s[9], s[14], m[8], m[9], m[10], m[11], m[12], m[13], m[14], m[15])
 #define XFG_B3_ROUND_Z(m, Z)                                                                         \
     do {                                                                                             \
         b3_half<(Z) & 0xFFu>(s[0], s[4], s[8], s[12], s[1], s[5], s[9], s[13], s[2], s[6], s[10], s[14],  \
                              s[3], s[7], s[11], s[15], m[0], m[1], m[2], m[3], m[4], m[5], m[6], m[7]);   \
-        b3_half<((Z) >> 8) & 0xFFu>(s[0], s[5], s[10], s[15], s[1], s[6], s[11], s[12], s[2], s[7], s[8], \
-                                    s[13], s[3], s[4], s[9], s[14], m[8], m[9], m[10], m[11], m[12], m[13], \
-                                    m[14], m[15]);                                                   \
+        XFG_B3_DIAG_Z(m, Z);                                                                         \
     } while (0)
 #else
+#define XFG_B3_DIAG_Z(m, Z) XFG_B3_DIAG_C(m)
 #define XFG_B3_ROUND_Z(m, Z) XFG_B3_ROUND_C(m)
 #endif
 
@@ -138,7 +148,17 @@ __host__ __device__ __forceinline__ void b3_compress(const uint32_t cv[8], uint3
                       (uint32_t)counter, (uint32_t)(counter >> 32), block_len, flags};
     constexpr unsigned Z2 = b3_perm_mask(ZM), Z3 = b3_perm_mask(Z2), Z4 = b3_perm_mask(Z3),
                        Z5 = b3_perm_mask(Z4), Z6 = b3_perm_mask(Z5), Z7 = b3_perm_mask(Z6);
-    XFG_B3_ROUND_C(m); XFG_B3_PERMUTE(m);
+    // round 1: the column half in C (the IV / counter / flag words of the state fold into it); the
+    // diagonal half as a block too, unless a column G had no message (both words zero): its outputs
+    // are then compile-time constants the C diagonal half folds (short element hashes)
+    constexpr bool col_const = (ZM & 0x03u) == 0x03u || (ZM & 0x0Cu) == 0x0Cu || (ZM & 0x30u) == 0x30u ||
+                               (ZM & 0xC0u) == 0xC0u;
+    XFG_B3_COL_C(m);
+    if constexpr (col_const)
+        XFG_B3_DIAG_C(m);
+    else
+        XFG_B3_DIAG_Z(m, ZM);
+    XFG_B3_PERMUTE(m);
     XFG_B3_ROUND_Z(m, Z2); XFG_B3_PERMUTE(m);
     XFG_B3_ROUND_Z(m, Z3); XFG_B3_PERMUTE(m);
     XFG_B3_ROUND_Z(m, Z4); XFG_B3_PERMUTE(m);
