@@ -8,4 +8,4 @@ mkdir -p gpurun_out/b3z
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/b3z/gputest.log 2>&1; rc=$?
 tail -2 gpurun_out/b3z/gputest.log
 [ $rc = 0 ] || exit $rc
-NO_LDE=1 REPS=${REPS:-3} LIBS="xfg-stark_amd/libxfgstark.so build/libxfgstark_head.so build/libxfgstark_cs.so" bash scripts/lib_ab.sh 2>&1 | tee gpurun_out/b3z/lib_ab.txt
+NO_LDE=1 REPS=${REPS:-3} LIBS="${LIBS:-xfg-stark_amd/libxfgstark.so build/libxfgstark_head.so build/libxfgstark_cs.so}" bash scripts/lib_ab.sh 2>&1 | tee gpurun_out/b3z/lib_ab.txt

@@ -250,6 +250,34 @@ __global__ __launch_bounds__(256) void leaves_lde_kernel(const u64* lde, Digest*
     block_tree_up(top, nodes, n / 2, lds, wmin);
 }
 
+// one LDE row per thread: the row's 2^LOGB-leaf subtree (top at heap level log2(beta), not stored),
+// then through LDS the row-pair level (heap n/2 + m/2) and one more (n/4 + m/4): 256 rows -> 64 nodes
+// per block, n/4 left for launch_tree_top. Against leaves_lde_kernel (two rows per thread) a thread
+// holds one row and one pending digest per subtree level -- 49-56 instead of 83-105 VGPRs, 8
+// instead of 4-5 waves per SIMD -- for the same compressions: the trace leaves 3.3 % faster, the
+// composition leaves unchanged (profiles/r05/leaves_row.txt).
+template <int NC, int LOGB>
+__global__ __launch_bounds__(256) void leaves_row_kernel(const u64* lde, Digest* nodes_all, u64 node_stride,
+                                                         int logn) {
+    __shared__ Digest lds[256];
+    const u64 n = 1ULL << logn;
+    const int proof = blockIdx.y, t = threadIdx.x;
+    const u64 m = (u64)blockIdx.x * 256 + t;
+    const u64* base = lde + (u64)proof * NC * (1 << LOGB) * n;
+    Digest d = lde_subtree<NC, LOGB, LOGB, 0>(base, n, m, nullptr);
+    Digest* nodes = nodes_all + (u64)proof * node_stride;
+    u64 c = n / 2;
+    for (int w = 128; w >= 64; w >>= 1, c >>= 1) {
+        lds[t] = d;
+        __syncthreads();
+        if (t < w) {
+            d = b3_merge(lds[2 * t], lds[2 * t + 1]);
+            nodes[c + (u64)blockIdx.x * w + t] = d;
+        }
+        __syncthreads();
+    }
+}
+
 // openings: recompute the local subtree heaps of selected rows; entry e = proof << logn | m
 template <int NC, int LOGB>
 __global__ __launch_bounds__(64) void open_rows_kernel(const u64* lde, const u64* entries, u64 count, Digest* out,
@@ -277,6 +305,16 @@ static int up_wmin(u64 T) { return (int)std::min<u64>(T, 64); }
 u64 launch_leaves_lde(const u64* lde, int nc, Digest* nodes, u64 node_stride, int npoly, int logn, int logbeta,
                       hipStream_t s) {
     const u64 n = 1ULL << logn, T = std::min<u64>(256, n / 2);
+#ifndef XFG_LEAVES_PAIR
+    if (n >= 1024) {
+        dim3 g((unsigned)(n / 256), npoly), b(256);
+        if (nc == 7) { XFG_LOGB_DISPATCH(leaves_row_kernel, 7, logbeta, g, b, 0, s, lde, nodes, node_stride, logn) }
+        else if (nc == 2) { XFG_LOGB_DISPATCH(leaves_row_kernel, 2, logbeta, g, b, 0, s, lde, nodes, node_stride, logn) }
+        else { XFG_LOGB_DISPATCH(leaves_row_kernel, 1, logbeta, g, b, 0, s, lde, nodes, node_stride, logn) }
+        XFG_CHECK_LAUNCH();
+        return n / 4;
+    }
+#endif
     const int wmin = up_wmin(T);
     dim3 g((unsigned)(n / 2 / T), npoly), b((unsigned)T);
     if (nc == 7) { XFG_LOGB_DISPATCH(leaves_lde_kernel, 7, logbeta, g, b, 0, s, lde, nodes, node_stride, logn, wmin) }
