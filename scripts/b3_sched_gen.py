@@ -125,6 +125,8 @@ def schedule(oname, nop, z=0):
 
 VARIANTS = [(o, n) for o in ("gbyg", "lock", "pairs", "lockxr", "stag1", "stag2", "stag3", "alt")
             for n in ("none", "slow", "fast", "fast1", "fs", "sf", "ff", "dep", "all")]
+if __import__("os").environ.get("B3_VARIANTS"):  # e.g. B3_VARIANTS="alt/fast alt/none" (a shorter ubench)
+    VARIANTS = [tuple(v.split("/")) for v in __import__("os").environ["B3_VARIANTS"].split()]
 
 
 def ubench_source(path):

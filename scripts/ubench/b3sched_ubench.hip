@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #define KB_PROLOGUE                                                                                  \
     uint32_t s0 = threadIdx.x, s1 = s0 * 3, s2 = s0 * 5, s3 = s0 * 7, s4 = s0 + 1, s5 = s0 + 2,      \
              s6 = s0 + 3, s7 = s0 + 4, s8 = s0 ^ 9, s9 = s0 ^ 10, s10 = s0 ^ 11, s11 = s0 ^ 12,      \
@@ -32,9 +33,9 @@
         s0 ^ s1 ^ s2 ^ s3 ^ s4 ^ s5 ^ s6 ^ s7 ^ s8 ^ s9 ^ s10 ^ s11 ^ s12 ^ s13 ^ s14 ^ s15;
 #include "b3sched_gen.inc"
 
-int main() {
+int main(int argc, char** argv) {
     uint32_t* d;
-    const int threads = 256, iters = 64;
+    const int threads = 256, iters = argc > 1 ? atoi(argv[1]) : 64;  // 64: ~1 ms per launch at 8 waves
     (void)hipMalloc(&d, (size_t)256 * 8 * threads * 4);
     const int waves_per_simd[] = {4, 5, 6, 8};
     for (auto& k : kbs) hipLaunchKernelGGL(k.f, dim3(2048), dim3(threads), 0, 0, d, iters);  // clocks up
