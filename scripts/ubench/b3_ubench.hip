@@ -1,6 +1,7 @@
 // Microbenchmark: BLAKE3 single-block compressions per second on gfx950 (independent chains)
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include "../../xfg-stark_amd/csrc/blake3.hpp"
 using namespace xfg;
 template <int CHAINS>
@@ -16,9 +17,9 @@ __global__ __launch_bounds__(256) void kb(Digest* out, int iters) {
     for (int c = 1; c < CHAINS; c++) for (int i = 0; i < 8; i++) r.w[i] ^= d[c].w[i];
     out[blockIdx.x * blockDim.x + threadIdx.x] = r;
 }
-int main() {
+int main(int argc, char** argv) {
     Digest* d;
-    const int blocks = 256 * 8, threads = 256, iters = 64;
+    const int blocks = 256 * 8, threads = 256, iters = argc > 1 ? atoi(argv[1]) : 64;
     hipMalloc(&d, (size_t)blocks * threads * sizeof(Digest));
     for (int v = 0; v < 3; v++) {
         hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
