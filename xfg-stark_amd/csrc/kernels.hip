@@ -355,21 +355,27 @@ __global__ __launch_bounds__(256) void tree_top_kernel(Digest* nodes_all, u64 no
     if (cs.kind != CoinStep::NONE && tid < 64) coin_root_step(cs, blockIdx.x, count > 1 ? lds[0] : nodes[1]);
 }
 // middle levels: a block merges 512 consecutive nodes of level `count` (two per thread, coalesced)
-// and continues through LDS down to one node, writing every parent: count / 512 nodes remain
+// and continues through LDS while a level keeps full waves, writing every parent: 64 nodes per block,
+// count / 8 remain. (Merging on down to one node per block ran six more levels on one part-filled
+// wave each: 13 wave-compressions per block for the work of 8.)
+#ifdef XFG_TREE_MID_TO_ONE  // A/B: the previous 512 -> 1 blocks
+constexpr int TREE_MID_WMIN = 1, TREE_MID_SHRINK = 512;
+#else
+constexpr int TREE_MID_WMIN = 64, TREE_MID_SHRINK = 8;
+#endif
 __global__ __launch_bounds__(256) void tree_mid_kernel(Digest* nodes_all, u64 node_stride, u64 count) {
     __shared__ Digest lds[256];
     Digest* nodes = nodes_all + (u64)blockIdx.y * node_stride;
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
     const Digest d = b3_merge(nodes[count + 2 * i], nodes[count + 2 * i + 1]);
     nodes[count / 2 + i] = d;
-    block_tree_up(d, nodes, count / 2, lds, 1);
+    block_tree_up(d, nodes, count / 2, lds, TREE_MID_WMIN);
 }
 void launch_tree_top(Digest* nodes, u64 node_stride, u64 count, int npoly, hipStream_t s, const CoinStep& cs) {
-    // one launch per 9 levels instead of one per level
     while (count > 512) {
         hipLaunchKernelGGL(tree_mid_kernel, dim3((unsigned)(count / 512), npoly), dim3(256), 0, s, nodes, node_stride,
                            count);
-        count /= 512;
+        count /= TREE_MID_SHRINK;
     }
     if (count > 1 || cs.kind != CoinStep::NONE) {
         int threads = (int)(count / 2);
