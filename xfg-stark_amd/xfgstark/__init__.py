@@ -448,10 +448,12 @@ class PendingBatch:
         self._release()
         return need
 
-    def __del__(self):
+    def __del__(self, _finalizing=sys.is_finalizing):
         # the workers write into this batch's buffers: never release them before the batch is done;
-        # a batch that was waited for but never consumed returns its buffer to the pool
-        if not sys.is_finalizing() and getattr(self._p, "_ctx", None):
+        # a batch that was waited for but never consumed returns its buffer to the pool (the
+        # finalizing check is bound at definition: module globals, `sys` included, are gone late in
+        # interpreter teardown)
+        if not _finalizing() and getattr(self._p, "_ctx", None):
             if self._res is None and not hasattr(self, "_wst"):
                 _lib.xfg_batch_wait(self._p._ctx, self._t)
             self._release()
@@ -480,10 +482,11 @@ class XfgBurnMintProver:
             _lib.xfg_ctx_destroy(self._ctx)
             self._ctx = None
 
-    def __del__(self):
-        # at interpreter exit the module globals (and the HIP runtime) may already be gone; process
-        # teardown releases the device buffers, so only collect contexts dropped while running
-        if not sys.is_finalizing():
+    def __del__(self, _finalizing=sys.is_finalizing):
+        # at interpreter exit the module globals (`sys` and the HIP runtime included) may already be
+        # gone -- hence the check bound at definition; process teardown releases the device buffers,
+        # so only collect contexts dropped while running
+        if not _finalizing():
             self.close()
 
     def _err(self, st):
