@@ -16,6 +16,8 @@ throughput, GPU vs host threads) and `cpu_baseline` (the oracle C restatement on
 import argparse
 import json
 import os
+import resource
+import socket
 import sys
 import time
 
@@ -129,6 +131,12 @@ class Exchange:
             self.recv_host = [_pinned(self.rows * self.rec, device).view(self.rows, self.rec)
                               for _ in range(recv_slots)]
             self.recv_dev = torch.empty((self.rows, self.rec), dtype=torch.uint8, device=device) if self.cuda else None
+            # device path: the other rows' length headers and the longest proof of each gather
+            # (_pack_d2h); the ring slot then holds the packed [rows - 1, per, maxlen] block
+            self.recv_hdr = [_pinned((self.rows - 1) * self.hdr, device).view(self.rows - 1, self.hdr)
+                             for _ in range(recv_slots)] if self.cuda and self.rows > 1 else None
+            self.packed_len = [0] * recv_slots
+        self.d2h_bytes_last = 0
         self.lookahead = max(1, lookahead)
         ring = self.lookahead + 1
         self.in_host = [_pinned(per * REC, device).view(per, REC) for _ in range(ring)]
@@ -261,7 +269,7 @@ class Exchange:
                 got = [self.recv_dev.view(-1)] if emul else (list(self.recv_dev.unbind(0)) if self.rank == 0 else None)
                 self._coll(self.side, self.dist.gather, self.send_dev, got, dst=0, group=self.group)
                 if self.rank == 0 and self.rows > 1:
-                    self._copy(self.side, self.recv_host[r][1:], self.recv_dev[1:])
+                    self._pack_d2h(r)
             else:
                 got = list(self.recv_host[r].unbind(0)) if self.rank == 0 else None
                 self._coll(None, self.dist.gather, self.send[s], got, dst=0, group=self.group)
@@ -269,6 +277,25 @@ class Exchange:
         self.send_busy[s] = h
         self.send_owned[s] = False
         return Gathered(self, h, r, s)
+
+    def _pack_d2h(self, r):
+        """rank 0, after a gather: bring the other rows' proofs to the host packed. The rows' length
+        headers come first (a few KB); every proof slot of the gathered records is then cut to the
+        longest proof actually present and the [rows - 1, per, maxlen] block is packed on the device
+        (one copy kernel on the side stream) and copied D2H -- instead of the records' full
+        proof-size-bound slots (each sized for the worst-case opening)"""
+        import numpy as np
+        rows = self.rows - 1
+        hdr = self.recv_hdr[r]
+        self._copy(self.side, hdr, self.recv_dev[1:, :self.hdr])
+        lens = hdr.numpy().view(np.int64)
+        maxlen = int(min(max(int(lens.max()), 0), self.cap))
+        self.packed_len[r] = maxlen
+        if maxlen:
+            src = self.recv_dev[1:, self.hdr:].view(rows, self.per, self.cap)[:, :, :maxlen]
+            dst = self.recv_host[r].view(-1)[:rows * self.per * maxlen].view(rows, self.per, maxlen)
+            self._copy(self.side, dst, src)
+        self.d2h_bytes_last = rows * self.hdr + rows * self.per * maxlen
 
     def drain(self):
         for h in self.send_busy + [p[1] for p in self.in_pending if p]:
@@ -308,14 +335,22 @@ class Gathered:
         allb = ex.recv_host[self.slot].numpy()
         out = []
         for q in range(ex.rows):
-            # rank 0's own record never left its host memory (CUDA path): read it from the send record
-            row = ex.send[self.send_slot].numpy() if q == 0 and ex.cuda else allb[q]
-            mv = memoryview(row)
-            for i, ln in enumerate(row[:ex.hdr].view(np.int64)):
-                if not 0 < ln <= ex.cap:
+            if q == 0 and ex.cuda:
+                # rank 0's own record never left its host memory: read it from the send record
+                row = ex.send[self.send_slot].numpy()
+                lens, body, slot = row[:ex.hdr].view(np.int64), row[ex.hdr:], ex.cap
+            elif ex.cuda:  # packed by _pack_d2h: headers apart, slots cut to the longest proof
+                slot = ex.packed_len[self.slot]
+                lens = ex.recv_hdr[self.slot][q - 1].numpy().view(np.int64)
+                body = allb.reshape(-1)[(q - 1) * ex.per * slot:q * ex.per * slot]
+            else:
+                row = allb[q]
+                lens, body, slot = row[:ex.hdr].view(np.int64), row[ex.hdr:], ex.cap
+            mv = memoryview(body)
+            for i, ln in enumerate(lens):
+                if not 0 < ln <= min(slot, ex.cap):
                     raise RuntimeError(f"exchange: rank {q} proof {i} has no proof in its record (length {ln})")
-                off = ex.hdr + i * ex.cap
-                out.append(mv[off:off + int(ln)])
+                out.append(mv[i * slot:i * slot + int(ln)])
         return out
 
 
@@ -449,6 +484,26 @@ def config5(prover, gpu, batch=4, calls=12, depth=6):
             "trace_lde_1proof_frac": round(lde_b / batch / (lde1_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
             "trace_lde_traffic": pmc["traffic_bytes"] if pmc else None, "traffic_source": src,
             "device_bytes_added": int(used), "proofs_in_flight": batch * depth}
+
+
+def single_proof(prover, n, reps=10, source=0):
+    """latency of one proof (BASELINE configs[1] at n = 2^16): xfg_prove_burn_mint called
+    synchronously, best of `reps` after one warm call, and the library's stage split of one more call
+    (XFG stage timers: host marshalling, each GPU stage, host replay and serialisation)"""
+    kw = synthetic.burn_inputs(source)
+    prover.prove_burn_mint(**kw, trace_length=n)
+    times = []
+    for _ in range(reps):
+        t = time.perf_counter()
+        prover.prove_burn_mint(**kw, trace_length=n)
+        times.append((time.perf_counter() - t) * 1e3)
+    prover.set_timing(True)
+    prover.prove_burn_mint(**kw, trace_length=n)
+    stages = {k: round(v, 3) for k, v in prover.stage_times().items()}
+    prover.set_timing(False)
+    return {"workload": f"configs[1]: one burn proof, {n}-step trace, blowup {BLOWUP}, xfg_prove_burn_mint "
+                        "(synchronous)", "ms": round(min(times), 3), "median_ms": round(sorted(times)[reps // 2], 3),
+            "reps": reps, "stage_ms": stages}
 
 
 def whole_proof_line(proofs_per_s, n, world):
@@ -626,18 +681,86 @@ def _free_port():
     return port
 
 
-def launch_ranks(gpus, argv):
+def launch_ranks(gpus, argv, limit_s=None):
     """`bench.py --gpus N` (N > 1) without a launcher: start N ranks with torch.distributed.run as a
     CHILD process (this process never touches the GPU, so nothing is exec'd from a GPU-initialised
     process), relay rank 0's JSON line to stdout and everything else to stderr, and return the child's
-    exit code. Reference harness: src/benchmarks/mod.rs:301-342."""
+    exit code. The child runs in its own process group: if this process is interrupted, or the ranks
+    outlive `limit_s` seconds (XFG_BENCH_LIMIT_S, default none), the whole group is terminated (then
+    killed) and a non-zero code returned, so no torchrun or rank is left behind. Reference harness:
+    src/benchmarks/mod.rs:301-342."""
+    import signal
     import subprocess
+    import threading
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + argv
-    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1)
-    for line in p.stdout:
-        print(line, end="", file=sys.stdout if line.lstrip().startswith("{") else sys.stderr, flush=True)
-    return p.wait()
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1, start_new_session=True)
+    expired = threading.Event()
+
+    def stop():
+        if p.poll() is not None:
+            return
+        for sig, wait in ((signal.SIGTERM, 15), (signal.SIGKILL, 15)):
+            try:
+                os.killpg(p.pid, sig)
+            except ProcessLookupError:
+                return
+            try:
+                p.wait(timeout=wait)
+                return
+            except subprocess.TimeoutExpired:
+                pass
+
+    def expire():
+        expired.set()
+        stop()
+    limit_s = limit_s if limit_s is not None else float(os.environ.get("XFG_BENCH_LIMIT_S", "0"))
+    timer = threading.Timer(limit_s, expire) if limit_s > 0 else None
+    if timer is not None:
+        timer.daemon = True
+        timer.start()
+    try:
+        for line in p.stdout:
+            print(line, end="", file=sys.stdout if line.lstrip().startswith("{") else sys.stderr, flush=True)
+        rc = p.wait()
+    finally:
+        if timer is not None:
+            timer.cancel()
+        stop()
+    if expired.is_set():
+        print(f"bench.py: ranks still running after {limit_s:.0f} s, terminated", file=sys.stderr)
+        return rc or 124
+    return rc
+
+
+def rank_cpus(local_rank, local_world, cpus):
+    """the host CPUs of one rank when `local_world` ranks share this node: a disjoint, contiguous slice
+    of the CPUs this process may run on (`cpus`), so the ranks' lane workers and host pools do not
+    migrate across each other; all of `cpus` when there are fewer CPUs than ranks"""
+    cpus = sorted(cpus)
+    k = len(cpus) // max(1, local_world)
+    if local_world <= 1 or k == 0:
+        return cpus
+    return cpus[local_rank * k:(local_rank + 1) * k]
+
+
+def host_threads_for(ncpus):
+    """XFG_HOST_THREADS for a rank with `ncpus` CPUs: the library's default 8 on a 16-CPU share (the
+    other half runs the lane workers), fewer on a smaller share"""
+    return max(2, min(8, ncpus // 2))
+
+
+def pin_rank(env):
+    """pin this rank (before torch or HIP start any thread) to its slice of the node's CPUs and size
+    the library's host pool to it, unless the caller set XFG_HOST_THREADS; -> the slice"""
+    if not hasattr(os, "sched_setaffinity"):
+        return None
+    local_world = int(env.get("LOCAL_WORLD_SIZE", env.get("WORLD_SIZE", "1")))
+    mine = rank_cpus(int(env.get("LOCAL_RANK", "0")), local_world, os.sched_getaffinity(0))
+    if local_world > 1:
+        os.sched_setaffinity(0, mine)
+        env.setdefault("XFG_HOST_THREADS", str(host_threads_for(len(mine))))
+    return mine
 
 
 def check_world(gpus, env):
@@ -675,6 +798,7 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = check_world(args.gpus, os.environ)
+    cpus = pin_rank(os.environ)
 
     import torch
     rank = int(os.environ.get("RANK", "0"))
@@ -687,7 +811,9 @@ def main():
     if world > 1 or args.dist:
         import torch.distributed as dist
         torch.cuda.set_device(gpu)
-        dist.init_process_group(backend)
+        # nccl: bind the communicator to this rank's GPU up front (without device_id RCCL guesses
+        # the device from the global rank and warns that a wrong guess can hang)
+        dist.init_process_group(backend, **({"device_id": torch.device("cuda", gpu)} if backend == "nccl" else {}))
     device = torch.device("cuda", gpu) if backend == "nccl" else torch.device("cpu")
 
     import xfgstark
@@ -735,11 +861,23 @@ def main():
                         packed[:args.warmup] if packed else None)
     barrier()
     prover.lde_probe(True)  # HIP events around every trace-LDE launch set inside the timed steps
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
     t0 = time.perf_counter()
     out = pipelined_steps(submit_fn, collect_fn, batches[args.warmup:], args.depth, ex,
                           packed[args.warmup:] if packed else None)
     barrier()
     el = time.perf_counter() - t0
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
+    # this rank's host load over the timed window: CPU seconds (all threads) per step and per second
+    mine = {"rank": rank, "device": gpu, "host": socket.gethostname(), "cpus": len(cpus) if cpus else None,
+            "cpu_first": min(cpus) if cpus else None,
+            "host_threads": int(os.environ.get("XFG_HOST_THREADS", "8")),
+            "cpu_s_per_step": round((ru1.ru_utime + ru1.ru_stime - ru0.ru_utime - ru0.ru_stime) / args.steps, 5),
+            "cpu_util": round((ru1.ru_utime + ru1.ru_stime - ru0.ru_utime - ru0.ru_stime) / el, 2)}
+    ranks = [mine]
+    if dist is not None:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
     if os.environ.get("XFG_BENCH_TIMELINE"):  # the window in the profiler's clock (CLOCK_MONOTONIC ns)
         print(f"window ns: {int(t0 * 1e9)} {int((t0 + el) * 1e9)}", file=sys.stderr)
     el_t = torch.tensor([el], dtype=torch.float64, device=device)
@@ -780,6 +918,10 @@ def main():
     t = time.perf_counter()
     prover.prove_batch(batches[-1][:per], trace_length=n)
     sync_call_ms = (time.perf_counter() - t) * 1e3
+
+    # BASELINE configs[1]: ONE proof of this shape through xfg_prove_burn_mint, synchronous (the
+    # reference's prove_burn_mint, src/burn_mint_prover.rs:62-129): best of 10 after a warm call
+    single = single_proof(prover, n)
 
     # ---- roofline: trace LDE kernel pair, algorithmic bytes 8*w*(n+N) per proof, timed over a window
     # of >= 150 ms of back-to-back launch sets: the chip's clock settles only after ~30 ms of load
@@ -825,7 +967,14 @@ def main():
             "sequencing": "one host worker thread (own process group, high-priority streams), "
                           "collectives in step order; no cross-stream waits on the GPU",
             "record_bytes_per_rank": ex.rec, "proof_size_bound": ex.cap,
-            "records_received_per_step": ex.rows},
+            "records_received_per_step": ex.rows,
+            # what the collectives saw: the world size and every rank's (rank, device, host) as
+            # all-gathered over the process group, and the bytes rank 0 copied D2H per step
+            "world": world, "ranks": [[r["rank"], r["device"], r["host"]] for r in ranks],
+            "d2h_bytes_per_step": ex.d2h_bytes_last, "d2h_bytes_unpacked": (ex.rows - 1) * ex.rec},
+        # every rank's host CPU over the timed window (getrusage, all threads): whether the host was
+        # the limit of a rank (cpu_util near its `cpus`)
+        "host_load": ranks,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
                      "traffic_source": traffic_src,
@@ -843,6 +992,7 @@ def main():
         "verify": vrate,
         "stage_ms_one_batch": prover_stage,
         "sync_prove_batch_ms": round(sync_call_ms, 3),
+        "single_proof": single,
     }
     if c5:
         line["config5"] = c5

@@ -167,12 +167,21 @@ def round_masks(zm):
     return out
 
 
-def product_header(path):
+def product_masks():
+    """every 8-bit half-round zero mask the device compression reaches: round 1's diagonal half
+    (message words 8..15 of the entry mask; round 1's column half stays in C) and both halves of
+    rounds 2..7"""
     masks = {0}
     for zm in ZERO_PATTERNS:
+        masks.add(zm >> 8)
         for z in round_masks(zm):
             masks.add(z & 0xFF)
             masks.add(z >> 8)
+    return masks
+
+
+def product_header(path):
+    masks = product_masks()
     ops = ('"+v"(a0), "+v"(b0), "+v"(c0), "+v"(d0), "+v"(a1), "+v"(b1), "+v"(c1), "+v"(d1), "+v"(a2), '
            '"+v"(b2), "+v"(c2), "+v"(d2), "+v"(a3), "+v"(b3), "+v"(c3), "+v"(d3) : "v"(x0), "v"(y0), "v"(x1), '
            '"v"(y1), "v"(x2), "v"(y2), "v"(x3), "v"(y3)')

@@ -4,7 +4,9 @@ Hash KATs are published vectors (BLAKE3 spec test vectors, Keccak-256) plus the 
 KAT (src/lib.rs:135-161); they are typed in here as data and checked against the oracle, never
 produced by it. Proof fixtures ARE produced by the oracle (parity unpinned against real
 Winterfell: see oracle/oracle.h) and pin the restatement against regressions and the GPU path.
-Usage: python tests/golden/make_golden.py
+Usage: python tests/golden/make_golden.py            (hash KATs, reference KATs, proofs.json)
+       python tests/golden/make_golden.py --configs  (config_proofs.json: the benchmark shapes, ~10 min
+                                                      on 8 processes)
 """
 import hashlib
 import json
@@ -106,7 +108,46 @@ def proof_fixtures():
     return out
 
 
+# BASELINE configs[2]: the 128 proofs test_config2_full_batch_in_flight makes (two 64-proof batches,
+# synthetic.burn_inputs(0..127), n = 2^16, blowup 8, reference options 42/8/4/None/8/31)
+C2_N, C2_COUNT = 1 << 16, 128
+# BASELINE configs[4] as bench.py's config5() and test_config5_quadratic_2p20_blowup16 run it:
+# n = 2^20, blowup 16, quadratic extension, 24 queries, grinding 4, folding 8, remainder 31
+C5_N, C5_SOURCE = 1 << 20, 5005
+C5_OPTIONS = {"blowup": 16, "field_extension": 2, "num_queries": 24}
+
+
+def _prove_digest(args):
+    src, n, extra = args
+    kw = synthetic.burn_inputs(src)
+    st, air = O.air_from_inputs(kw["burn_amount"], kw["mint_amount"], kw["tx_prefix_hash"],
+                                kw["recipient_address"], kw["secret"], kw["network_id"],
+                                kw["target_chain_id"], kw["commitment_version"])
+    assert st == 0
+    opts = O.options(**extra)
+    st, proof = O.prove(air, n, opts)
+    assert st == 0 and O.verify(air, proof, opts) == 0, (src, n)
+    return {"source": src, "len": len(proof), "sha256": hashlib.sha256(proof).hexdigest()}
+
+
+def config_fixtures(procs=8):
+    """digests of whole oracle proofs at the benchmark shapes (the oracle is single-threaded per
+    proof, so the 128 configs[2] proofs run on a process pool)"""
+    import multiprocessing as mp
+    with mp.get_context("fork").Pool(procs) as pool:
+        c5 = pool.apply_async(_prove_digest, ((C5_SOURCE, C5_N, C5_OPTIONS),))
+        c2 = pool.map(_prove_digest, [(i, C2_N, {}) for i in range(C2_COUNT)], chunksize=1)
+        c5 = c5.get()
+    print("config5", c5["len"], c5["sha256"][:16])
+    return {"config2_batch": {"n": C2_N, "blowup": 8, "options": {}, "proofs": c2},
+            "config5": dict(c5, n=C5_N, blowup=16, options={k: v for k, v in C5_OPTIONS.items() if k != "blowup"})}
+
+
 def main():
+    if "--configs" in sys.argv:
+        with open(os.path.join(HERE, "config_proofs.json"), "w") as f:
+            json.dump(config_fixtures(), f, indent=1)
+        return
     for v in KATS["blake3"]:
         assert O.blake3(bytes.fromhex(v["input_hex"])).hex() == v["digest"], v
     for v in KATS["keccak256"]:

@@ -98,6 +98,22 @@ def test_every_block_is_four_g_functions():
             assert got[16:] == msg
 
 
+def test_every_reached_mask_has_its_block():
+    """every zero mask a device compression reaches (round 1's diagonal half and rounds 2..7 of each
+    entry pattern of the element hashes) has its own block, so no half-round silently falls back to
+    the generic Z = 0 block (the fallback is correct, only slower)"""
+    sys.path.insert(0, os.path.dirname(GEN))
+    import b3_sched_gen as G
+    have = set(blocks()) - {None}
+    for zm in G.ZERO_PATTERNS:
+        z, reached = zm, [zm >> 8]
+        for _ in range(6):
+            z = G.perm_mask(z)
+            reached += [z & 0xFF, z >> 8]
+        for r in reached:
+            assert r == 0 or r in have, f"entry mask {zm:#06x} reaches Z = {r:#04x} with no block"
+
+
 PERM = [2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8]
 IV = [0x6A09E667, 0xBB67AE85, 0x3C6EF372, 0xA54FF53A, 0x510E527F, 0x9B05688C, 0x1F83D9AB, 0x5BE0CD19]
 COL = [(0, 4, 8, 12), (1, 5, 9, 13), (2, 6, 10, 14), (3, 7, 11, 15)]

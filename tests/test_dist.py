@@ -29,7 +29,8 @@ def _fake_prove(kws):
 
 class _FakeRecordBatch:
     """a submitted batch writing into an exchange record like PendingBatch.record_ready: int64
-    lengths, then one FAKE_CAP slot per proof; `fail` = index of a proof that fails (length 0)"""
+    lengths, then one FAKE_CAP slot per proof; `fail` = index of a proof that fails (length 0), or
+    "batch": the whole batch fails (xfg_batch_wait's status; every length zeroed)"""
 
     def __init__(self, kws, record, fail=None):
         self.kws, (self.addr, self.nbytes, self.owner), self.fail = kws, record, fail
@@ -40,8 +41,10 @@ class _FakeRecordBatch:
         assert self.nbytes >= 8 * k + k * FAKE_CAP
         hdr = (C.c_int64 * k).from_address(self.addr)
         for i, p in enumerate(proofs):
-            hdr[i] = 0 if i == self.fail else len(p)
+            hdr[i] = 0 if self.fail in (i, "batch") else len(p)
             C.memmove(self.addr + 8 * k + i * FAKE_CAP, p, len(p))
+        if self.fail == "batch":
+            raise RuntimeError("batch failed")
         if self.fail is not None:  # as PendingBatch.record_ready: length zeroed, then raise
             raise RuntimeError(f"proof {self.fail} failed")
 
@@ -134,6 +137,36 @@ def test_exchange_failed_proof_raises_on_rank0():
     (r0, k0, m0), (r1, k1, m1) = _run(2, 2, expect=2, steps=3, depth=2, fail=1)
     assert (r0, k0, r1, k1) == (0, "error", 1, "error")
     assert "rank 1 proof 1" in m0 and m1 == "proof 1 failed"
+
+
+def test_exchange_batch_failure_raises_on_rank0():
+    """a whole batch that failed on another rank (every length zeroed by record_ready) is rejected
+    on rank 0 at its first proof, and the failing rank raises its own error"""
+    (r0, k0, m0), (r1, k1, m1) = _run(2, 2, expect=2, steps=2, depth=2, fail="batch")
+    assert (r0, k0, r1, k1) == (0, "error", 1, "error")
+    assert "rank 1 proof 0" in m0 and m1 == "batch failed"
+
+
+def test_record_ready_zeroes_lengths_on_batch_failure():
+    """PendingBatch.record_ready itself: when xfg_batch_wait fails for the whole batch (every
+    per-proof status 0, header words still at the capacity the submission wrote), every length in
+    the caller's record is zeroed before it raises; a per-proof failure zeroes only that proof"""
+    import xfgstark
+
+    class _P:
+        _free = []
+
+        def _err(self, st):
+            return xfgstark.XfgStarkError(st, "batch failed")
+
+    for wst, sts, want in ((7, [0, 0, 0], [0, 0, 0]), (0, [0, 5, 0], [4096, 0, 4096])):
+        lens = (C.c_int64 * 3)(4096, 4096, 4096)
+        st_arr = (C.c_int * 3)(*sts)
+        pb = xfgstark.PendingBatch(_P(), 0, None, 0, 4096, None, lens, st_arr, record=True)
+        pb._wst = wst  # as if xfg_batch_wait had returned it
+        with pytest.raises(xfgstark.XfgStarkError):
+            pb.record_ready()
+        assert list(lens) == want
 
 
 def test_pack_unpack_roundtrip():
@@ -323,6 +356,45 @@ def test_config3_eight_ranks_real_prover(tmp_path):
         assert st == 0 and got[q * per] == want, q
 
 
+def test_bench_launch_limit_kills_the_ranks(monkeypatch):
+    """a rank that hangs (here: a child that prints, then sleeps) is terminated with its whole
+    process group once the wall-clock limit passes, and launch_ranks returns non-zero"""
+    import subprocess
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    real, procs = subprocess.Popen, []
+
+    def hang(cmd, **kw):
+        p = real([sys.executable, "-c", "import time; print('rank up', flush=True); time.sleep(120)"], **kw)
+        procs.append(p)
+        return p
+
+    monkeypatch.setattr(subprocess, "Popen", hang)
+    t = time.time()
+    assert bench.launch_ranks(2, ["--steps", "1"], limit_s=2) != 0
+    assert time.time() - t < 30 and procs[0].poll() is not None
+
+
+def test_rank_cpu_slices():
+    """bench.py pins each rank of a node to a disjoint slice of the CPUs it may use (the driver's
+    8-GPU node: 8 ranks) and sizes the host pool to the slice"""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    cpus = set(range(16, 144))  # 128 CPUs, not starting at 0
+    sl = [bench.rank_cpus(r, 8, cpus) for r in range(8)]
+    assert all(len(x) == 16 for x in sl) and len(set().union(*map(set, sl))) == 128
+    assert sl[0][0] == 16 and sl[7][-1] == 143
+    assert bench.rank_cpus(0, 1, cpus) == sorted(cpus)           # one rank: everything
+    assert bench.rank_cpus(3, 8, {0, 1, 2}) == [0, 1, 2]          # fewer CPUs than ranks: no split
+    assert [bench.rank_cpus(r, 3, range(8)) for r in range(3)] == [[0, 1], [2, 3], [4, 5]]
+    assert [bench.host_threads_for(k) for k in (1, 2, 4, 16, 32)] == [2, 2, 2, 8, 8]
+
+
 def test_bench_gpus_mismatch_fails_loudly():
     """under a launcher, --gpus must equal WORLD_SIZE: a mismatch exits non-zero before any GPU work
     instead of printing a line for a different N"""
@@ -351,7 +423,10 @@ def test_bench_launch_command(monkeypatch):
             seen["cmd"] = cmd
             self.stdout = io.StringIO('torchrun chatter\n{"metric": "m", "n_gpus": 4}\n')
 
-        def wait(self):
+        def wait(self, timeout=None):
+            return 3
+
+        def poll(self):
             return 3
 
     monkeypatch.setattr(subprocess, "Popen", FakePopen)
@@ -387,6 +462,11 @@ def test_bench_gpus_two_without_launcher():
     assert len(lines) == 1
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["verified"] == 16 and line["config"]["proofs_per_step"] == 16
+    ex, load = line["exchange"], line["host_load"]
+    assert ex["world"] == 2 and [r[0] for r in ex["ranks"]] == [0, 1]
+    assert [r["rank"] for r in load] == [0, 1] and all(r["cpu_s_per_step"] > 0 for r in load)
+    if len(os.sched_getaffinity(0)) >= 2:  # two disjoint affinity slices
+        assert load[0]["cpu_first"] + load[0]["cpus"] <= load[1]["cpu_first"]
 
 
 @pytest.mark.gpu

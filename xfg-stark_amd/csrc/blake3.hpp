@@ -33,7 +33,7 @@ __host__ __device__ __forceinline__ uint32_t b3_rotr(uint32_t x, int n) { return
 // (profiles/r05/b3_vop3_ab.txt). Operands the compiler knows are constants keep the plain C form
 // so that it still folds them (the first round's IV words, zero message words).
 __host__ __device__ __forceinline__ uint32_t b3_xor(uint32_t a, uint32_t b) {
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(XFG_B3_VOP2)
+#if defined(__HIP_DEVICE_COMPILE__)
     if (__builtin_constant_p(a) || __builtin_constant_p(b)) return a ^ b;
     uint32_t r;
     asm("v_xor_b32_e64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
@@ -43,7 +43,7 @@ __host__ __device__ __forceinline__ uint32_t b3_xor(uint32_t a, uint32_t b) {
 #endif
 }
 __host__ __device__ __forceinline__ uint32_t b3_add(uint32_t a, uint32_t b) {
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(XFG_B3_VOP2)
+#if defined(__HIP_DEVICE_COMPILE__)
     if (__builtin_constant_p(a) || __builtin_constant_p(b)) return a + b;
     uint32_t r;
     asm("v_add_u32_e64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
@@ -112,7 +112,7 @@ __host__ __device__ constexpr unsigned b3_perm_mask(unsigned z) {
     return r;
 }
 
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(XFG_B3_VOP2) && !defined(XFG_B3_COMPILER_SCHED)
+#if defined(__HIP_DEVICE_COMPILE__)
 // The device rounds 2-7 issue in a fixed order: each half-round (four independent G functions, 48
 // VALU) is one asm block generated by scripts/b3_sched_gen.py -- fast and slow instructions of
 // different G's alternating, an s_nop after each fast one. gfx950 issues its two-source e64 xor / add
@@ -133,7 +133,7 @@ __host__ __device__ constexpr unsigned b3_perm_mask(unsigned z) {
                              s[3], s[7], s[11], s[15], m[0], m[1], m[2], m[3], m[4], m[5], m[6], m[7]);   \
         XFG_B3_DIAG_Z(m, Z);                                                                         \
     } while (0)
-#else
+#else  // host: the compiler's order
 #define XFG_B3_DIAG_Z(m, Z) XFG_B3_DIAG_C(m)
 #define XFG_B3_ROUND_Z(m, Z) XFG_B3_ROUND_C(m)
 #endif
@@ -146,7 +146,7 @@ __host__ __device__ __forceinline__ void b3_compress(const uint32_t cv[8], uint3
     uint32_t s[16] = {cv[0], cv[1], cv[2], cv[3], cv[4], cv[5], cv[6], cv[7],
                       XFG_B3_IV0, XFG_B3_IV1, XFG_B3_IV2, XFG_B3_IV3,
                       (uint32_t)counter, (uint32_t)(counter >> 32), block_len, flags};
-    constexpr unsigned Z2 = b3_perm_mask(ZM), Z3 = b3_perm_mask(Z2), Z4 = b3_perm_mask(Z3),
+    [[maybe_unused]] constexpr unsigned Z2 = b3_perm_mask(ZM), Z3 = b3_perm_mask(Z2), Z4 = b3_perm_mask(Z3),
                        Z5 = b3_perm_mask(Z4), Z6 = b3_perm_mask(Z5), Z7 = b3_perm_mask(Z6);
     // round 1: the column half in C (the IV / counter / flag words of the state fold into it); the
     // diagonal half as a block too, unless a column G had no message (both words zero): its outputs

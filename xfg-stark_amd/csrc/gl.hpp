@@ -159,45 +159,15 @@ __device__ __forceinline__ u64 gl_sub_u32(u64 lo, u32 h) {
     return gl_sub_weak(lo, h);
 #endif
 }
-// 64x64 -> 128 product as lo + (hi + cv 2^32) 2^64 from four v_mad_u64_u32 (8 VALU):
-// t1 = a0 b1 + (a0 b0 >> 32), t2 = a1 b0 + t1 (carry cv), lo = {lo(a0 b0), lo(t2)}, hi = a1 b1 + hi(t2)
-__device__ __forceinline__ void gl_prod(u64 a, u64 b, u64& lo, u64& hi, u32& cv) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    u64 p, x, t1, t2, s, c;
-    asm("v_mad_u64_u32 %[p], %[s], %[a0], %[b0], 0\n\t"
-        "v_lshrrev_b64 %[x], 32, %[p]\n\t"
-        "v_mad_u64_u32 %[t1], %[s], %[a0], %[b1], %[x]\n\t"
-        "v_mad_u64_u32 %[t2], %[c], %[a1], %[b0], %[t1]\n\t"
-        "v_pk_mov_b32 %[lo], %[p], %[t2] op_sel:[0,0]\n\t"
-        "v_lshrrev_b64 %[x], 32, %[t2]\n\t"
-        "v_mad_u64_u32 %[hi], %[s], %[a1], %[b1], %[x]\n\t"
-        "v_cndmask_b32_e64 %[cv], 0, 1, %[c]"
-        : [p] "=&v"(p), [x] "=&v"(x), [t1] "=&v"(t1), [t2] "=&v"(t2), [lo] "=&v"(lo), [hi] "=&v"(hi),
-          [cv] "=&v"(cv), [s] "=&s"(s), [c] "=&s"(c)
-        : [a0] "v"((u32)a), [a1] "v"((u32)(a >> 32)), [b0] "v"((u32)b), [b1] "v"((u32)(b >> 32)));
-#else
-    const unsigned __int128 m = (unsigned __int128)a * b;
-    lo = (u64)m;
-    hi = (u64)(m >> 64);
-    cv = 0;
-#endif
-}
-
 __host__ __device__ __forceinline__ u64 gl_mul(u64 a, u64 b) {
 #if defined(__HIP_DEVICE_COMPILE__)
     // a b = lo + hl 2^64 + (hh + c) 2^96 == lo - (hh + c) + hl EPS, (hh + c) <= 2^32 - 1 for any a, b
-    // < 2^64 (15 VALU + 1 SALU; gl_prod + gl_sub_weak + gl_fold was 18, the compiler's own lowering
+    // < 2^64 (15 VALU + 1 SALU; the round-4 product + gl_sub_weak + gl_fold was 18, the compiler's own lowering
     // of the same math 24). The product's carry c is never materialised: it is the borrow-in of the
     // subtraction lo - hh - c, done on the words of the partial products as they come out of the
     // mads (lo = (p.lo, t2.lo)), so neither the 64-bit assembly of lo nor hh + c costs an instruction;
     // a borrow out of the high word adds p (- EPS mod 2^64) once, then gl_fold adds hl EPS.
     // Each VALU-written carry / borrow mask is read by a VALU only after >= 2 wait states.
-#if defined(XFG_MUL_V1)  // A/B builds only: the round-4 form
-    u64 lo_, hi_;
-    u32 cv_;
-    gl_prod(a, b, lo_, hi_, cv_);
-    return gl_fold(gl_sub_weak(lo_, (u32)(hi_ >> 32) + cv_), (u32)hi_);
-#endif
     u64 p, t1, t2, hi, x, s, c;
     const u32 a0 = (u32)a, a1 = (u32)(a >> 32), b0 = (u32)b, b1 = (u32)(b >> 32);
     asm("v_mad_u64_u32 %[p], %[s], %[a0], %[b0], 0\n\t"

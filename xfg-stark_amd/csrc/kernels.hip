@@ -305,7 +305,6 @@ static int up_wmin(u64 T) { return (int)std::min<u64>(T, 64); }
 u64 launch_leaves_lde(const u64* lde, int nc, Digest* nodes, u64 node_stride, int npoly, int logn, int logbeta,
                       hipStream_t s) {
     const u64 n = 1ULL << logn, T = std::min<u64>(256, n / 2);
-#ifndef XFG_LEAVES_PAIR
     if (n >= 1024) {
         dim3 g((unsigned)(n / 256), npoly), b(256);
         if (nc == 7) { XFG_LOGB_DISPATCH(leaves_row_kernel, 7, logbeta, g, b, 0, s, lde, nodes, node_stride, logn) }
@@ -314,7 +313,6 @@ u64 launch_leaves_lde(const u64* lde, int nc, Digest* nodes, u64 node_stride, in
         XFG_CHECK_LAUNCH();
         return n / 4;
     }
-#endif
     const int wmin = up_wmin(T);
     dim3 g((unsigned)(n / 2 / T), npoly), b((unsigned)T);
     if (nc == 7) { XFG_LOGB_DISPATCH(leaves_lde_kernel, 7, logbeta, g, b, 0, s, lde, nodes, node_stride, logn, wmin) }
@@ -358,11 +356,7 @@ __global__ __launch_bounds__(256) void tree_top_kernel(Digest* nodes_all, u64 no
 // and continues through LDS while a level keeps full waves, writing every parent: 64 nodes per block,
 // count / 8 remain. (Merging on down to one node per block ran six more levels on one part-filled
 // wave each: 13 wave-compressions per block for the work of 8.)
-#ifdef XFG_TREE_MID_TO_ONE  // A/B: the previous 512 -> 1 blocks
-constexpr int TREE_MID_WMIN = 1, TREE_MID_SHRINK = 512;
-#else
 constexpr int TREE_MID_WMIN = 64, TREE_MID_SHRINK = 8;
-#endif
 __global__ __launch_bounds__(256) void tree_mid_kernel(Digest* nodes_all, u64 node_stride, u64 count) {
     __shared__ Digest lds[256];
     Digest* nodes = nodes_all + (u64)blockIdx.y * node_stride;

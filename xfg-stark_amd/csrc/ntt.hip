@@ -67,17 +67,8 @@ __device__ __forceinline__ u64 swap_lane_pair(u64 x) {
 // offset and no 64-bit address is computed per store (the odd lane stores output r + 1: its extra
 // `step` goes into its VGPR offset once)
 typedef u32 u32x4 __attribute__((__vector_size__(16)));
-#ifndef XFG_PAIR_STORES
-#define XFG_PAIR_STORES 1
-#endif
 template <int RR>
 __device__ __forceinline__ void store_pairs_buf(const u64* v, __amdgpu_buffer_rsrc_t rs, u32 vo, u32 step) {
-    if (!XFG_PAIR_STORES) {  // A/B build: one 8-byte store per output, no lane swap
-        const u32 vl = vo + (threadIdx.x & 1) * 8;
-#pragma unroll
-        for (int r = 0; r < RR; r++) buf_st(rs, vl, (u32)r * step, v[r]);
-        return;
-    }
     const bool odd = threadIdx.x & 1;
     const u32 vl = vo + (odd ? step : 0u);
 #pragma unroll

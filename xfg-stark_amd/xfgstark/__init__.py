@@ -409,7 +409,9 @@ class PendingBatch:
         self._consumed = "record_ready"
         st = self.wait()
         bad = [i for i in range(len(self._sts)) if self._sts[i]]
-        for i in bad:
+        # a batch-level failure leaves every status 0 and the header words at the capacity the
+        # submission wrote: zero them all, so the record cannot be read as cap-byte proofs
+        for i in (range(len(self._sts)) if st else bad):
             self._lens[i] = 0
         if st:
             raise self._p._err(st)
