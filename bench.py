@@ -292,6 +292,8 @@ class Exchange:
         maxlen = int(min(max(int(lens.max()), 0), self.cap))
         self.packed_len[r] = maxlen
         if maxlen:
+            # (measured against the full-row D2H: equal within noise at the emulated N = 8 load, and
+            # one hipMemcpy2DAsync per row instead of the copy kernel -30 %: profiles/r06/exchange_x8.txt)
             src = self.recv_dev[1:, self.hdr:].view(rows, self.per, self.cap)[:, :, :maxlen]
             dst = self.recv_host[r].view(-1)[:rows * self.per * maxlen].view(rows, self.per, maxlen)
             self._copy(self.side, dst, src)

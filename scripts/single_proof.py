@@ -34,6 +34,7 @@ def run(reps, calls_path):
     ms = [(b - a) * 1e3 for a, b in spans]
     print(f"single proof ms: best {min(ms):.3f} median {sorted(ms)[len(ms) // 2]:.3f} of {reps}")
     if calls_path:
+        os.makedirs(os.path.dirname(os.path.abspath(calls_path)), exist_ok=True)
         with open(calls_path, "w") as f:
             for a, b in spans:
                 f.write(f"{int(a * 1e9)} {int(b * 1e9)}\n")
