@@ -1694,33 +1694,6 @@ int xfg_bench_lde(xfg_ctx* c, uint32_t count, uint64_t n, uint32_t blowup, uint3
         }
         HIPCHK(hipMemcpy(L->coef.p, h.data(), h.size() * 8, hipMemcpyHostToDevice));
         launch_lde(L->coef.p, n, L->lde.p, L->scratch.p, count * 7, logn, logbeta, T, L->stream);  // warm
-#ifdef XFG_EXP_LDE_STREAMS  // experiment: the launch set split over S streams (pass A / B of different chunks overlap)
-        if (const char* sv = getenv("XFG_EXP_S")) {
-            const int S = atoi(sv), np = (int)count * 7, per = (np + S - 1) / S;
-            std::vector<hipStream_t> ss(S);
-            for (auto& st : ss) HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-            HIPCHK(hipDeviceSynchronize());
-            HIPCHK(hipEventRecord(L->ev[0], L->stream));
-            for (auto& st : ss) HIPCHK(hipStreamWaitEvent(st, L->ev[0], 0));
-            for (uint32_t i = 0; i < iters; i++)
-                for (int k = 0; k < S; k++) {
-                    const int p0 = k * per, cnt = std::min(per, np - p0);
-                    launch_lde(L->coef.p + (size_t)p0 * n, n, L->lde.p + (size_t)p0 * N, L->scratch.p + (size_t)p0 * N, cnt,
-                               logn, logbeta, T, ss[k]);
-                }
-            for (auto& st : ss) {
-                HIPCHK(hipEventRecord(L->ev[1], st));
-                HIPCHK(hipStreamWaitEvent(L->stream, L->ev[1], 0));
-            }
-            HIPCHK(hipEventRecord(L->ev[1], L->stream));
-            HIPCHK(hipEventSynchronize(L->ev[1]));
-            float ms = 0;
-            HIPCHK(hipEventElapsedTime(&ms, L->ev[0], L->ev[1]));
-            *avg_ms = ms / iters;
-            for (auto& st : ss) HIPCHK(hipStreamDestroy(st));
-            return XFG_OK;
-        }
-#endif
         HIPCHK(hipEventRecord(L->ev[0], L->stream));
         for (uint32_t i = 0; i < iters; i++)
             launch_lde(L->coef.p, n, L->lde.p, L->scratch.p, count * 7, logn, logbeta, T, L->stream);
