@@ -68,6 +68,20 @@ def test_lde_kernel_tile_paths_match_oracle(prover, n, blowup):
     assert np.array_equal(got, O.evaluate_lde_np(coef[0], blowup, 7))
 
 
+@pytest.mark.parametrize("npoly,blowup", [(32, 8), (32, 2), (33, 16), (28, 8)])
+def test_lde_launch_set_routes_match_oracle(prover, npoly, blowup):
+    """the two routes of the tabled 2^16 forward LDE: launch sets of >= 512 all-coset blocks (16 per
+    polynomial: 32 or 33 polynomials) take ntt_pass_a_cos2 (beta >= 4) / ntt_pass_a_cos (beta = 2) +
+    ntt_pass_b_tq, smaller ones (28: one proof's trace is 7) one block per (tile, poly, coset); both
+    bit-exact against the oracle on every polynomial"""
+    n = 1 << 16
+    rng = np.random.default_rng(npoly * 100 + blowup)
+    coef = rng.integers(0, P, size=(npoly, n), dtype=np.uint64)
+    got = np.asarray(prover.debug_lde(coef, n, blowup))
+    for k in range(npoly):
+        assert np.array_equal(got[k], O.evaluate_lde_np(coef[k], blowup, 7)), k
+
+
 @pytest.mark.parametrize("blowup", [8, 16])
 def test_lde_r1024_kernels_two_polys_match_oracle(prover, blowup):
     """ntt_pass_a_r1024 / ntt_pass_b_r1024 (n = 2^20 past the four-step tables): two polynomials, so

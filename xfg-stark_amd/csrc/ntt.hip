@@ -1103,8 +1103,14 @@ static void ntt_run(NttArgs& a, int npoly, bool inv, hipStream_t s) {
     }
     // pass A: all cosets of a column tile in one block where the four-step table exists (R = 256):
     // shift-twisted cosets (ntt_pass_a_cos2) for beta >= 4, per-coset pre-factors (ntt_pass_a_cos) at
-    // beta = 2; the four-step twiddles are then applied by pass B as it loads (tq_b)
-    if (a.t4 && a.logR == 8 && ltA == 8 && eA == 4 && !(a.xcd & 1)) {
+    // beta = 2; the four-step twiddles are then applied by pass B as it loads (tq_b). Only for launch
+    // sets of >= 512 such blocks (two per CU): the all-coset grid is C / 16 blocks per polynomial, so
+    // a small set (one proof's trace: 7 polynomials, its composition or DEEP column: 1) leaves most CUs
+    // idle while each block walks its beta cosets, and one block per (tile, poly, coset) -- ntt_pass_a,
+    // beta times the grid -- finishes sooner: 2^16 x 8, 1 / 7 / 16 / 28 polynomials 52 / 67 / 77 / 110 us
+    // against 20 / 41 / 66 / 107 us; 32 / 64 / 224 polynomials 119 / 232 / 727 against 122 / 255 / 821
+    // (profiles/r06/lde_small.txt)
+    if (a.t4 && a.logR == 8 && ltA == 8 && eA == 4 && !(a.xcd & 1) && (u64)npoly * (C >> logTC) >= 512) {
         a.tq_b = 1;
         if (a.logbeta >= 2)
             hipLaunchKernelGGL(ntt_pass_a_cos2, dim3(C >> logTC, npoly), dim3(256), lds_a, s, a);
