@@ -564,7 +564,10 @@ def test_gpu_batch_verify_node_vector_mutants(prover, ext):
     compaction) against the host verifier's BatchMerkleProof::get_root and the oracle verifier on
     openings whose node vectors parse but do not fit: the GPU, host and oracle verdicts are equal on
     every item, the misfits are rejected, an appended (unread) node is accepted as winter-crypto
-    0.8's get_root accepts it, and the untouched proofs stay accepted in the same batch"""
+    0.8's get_root accepts it, and the untouched proofs stay accepted in the same batch.
+    Pinned to the project's oracle restatement (oracle/orc_stark.c batch_root), not to an upstream
+    fixture: winter-crypto is not vendored in the reference, so the appended-node verdict is parity
+    unpinned against it"""
     import xfgstark
     o = xfgstark.ProofOptions.reference()
     o.field_extension = ext

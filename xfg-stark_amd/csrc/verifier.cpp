@@ -149,7 +149,11 @@ std::string parse_contents(ParsedProof& pf) {
 // level. Nodes past the ones the walk takes are ignored: winter-crypto 0.8's get_root consumes the
 // vectors through per-position pointers and never checks that every node was used (the oracle's
 // batch_root restates the same walk, oracle/orc_stark.c), so an opening with a trailing extra node
-// still verifies there, and here.
+// still verifies there, and here. PARITY UNPINNED against upstream: winter-crypto 0.8.x
+// (`BatchMerkleProof::get_root`, src/merkle/proofs.rs of that crate) is not vendored in the reference
+// and no reference fixture covers an over-long node vector, so this acceptance rests on the
+// restatement of its published walk (the per-position `proof_pointers` advance, no final check that
+// each vector was consumed); test_gpu_batch_verify_node_vector_mutants pins GPU = host = oracle only.
 bool merkle_symbolic(const std::vector<u64>& idx, const Paths& paths, u64 L, MerkleSym& out) {
     thread_local BatchOpening plan;
     plan_batch_opening(idx, L, plan);
