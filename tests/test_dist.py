@@ -167,6 +167,24 @@ def test_record_ready_zeroes_lengths_on_batch_failure():
         with pytest.raises(xfgstark.XfgStarkError):
             pb.record_ready()
         assert list(lens) == want
+        with pytest.raises(xfgstark.XfgStarkError):  # no views of a failed batch
+            pb.record_views()
+    # a successful batch: zero-copy views of each proof's used bytes in the caller's record
+    cap, k = 64, 3
+    rec = (C.c_uint8 * (8 * k + cap * k))()
+    lens = (C.c_int64 * k).from_buffer(rec)
+    body = [bytes([7 + i]) * (10 + 20 * i) for i in range(k)]
+    for i, b in enumerate(body):
+        lens[i] = len(b)
+        C.memmove(C.addressof(rec) + 8 * k + i * cap, b, len(b))
+    pb = xfgstark.PendingBatch(_P(), 0, None, C.addressof(rec) + 8 * k, cap, None, lens, (C.c_int * k)(), record=True,
+                               owner=rec)
+    pb._wst = 0
+    pb.record_ready()
+    views = pb.record_views()
+    assert [bytes(v) for v in views] == body
+    rec[8 * k] = 99  # views, not copies
+    assert views[0][0] == 99
 
 
 def test_pack_unpack_roundtrip():

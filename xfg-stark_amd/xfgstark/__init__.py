@@ -419,6 +419,14 @@ class PendingBatch:
             raise XfgStarkError(self._sts[bad[0]], STATUS.get(self._sts[bad[0]]))
         return 8 * len(self._sts) + self._cap * len(self._sts)
 
+    def record_views(self):
+        """after record_ready(): every proof of the batch as a zero-copy memoryview into the caller's
+        record (valid while the record is neither freed nor reused)"""
+        if self._consumed != "record_ready" or not hasattr(self, "_wst") or self._wst:
+            raise XfgStarkError(9, "record_views: call record_ready() first (and it must have succeeded)")
+        return [memoryview((C.c_uint8 * self._cap).from_address(self._base + i * self._cap)).cast("B")[:self._lens[i]]
+                for i in range(len(self._sts))]
+
     def packed_into(self, dst):
         """wait, then write the batch as one record into the uint8 numpy array `dst`: count int64
         lengths followed by the proof bytes back to back, straight from the workers' output buffer
