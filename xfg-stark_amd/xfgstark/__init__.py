@@ -422,7 +422,8 @@ class PendingBatch:
     def record_views(self):
         """after record_ready(): every proof of the batch as a zero-copy memoryview into the caller's
         record (valid while the record is neither freed nor reused)"""
-        if self._consumed != "record_ready" or not hasattr(self, "_wst") or self._wst:
+        if (self._consumed != "record_ready" or not hasattr(self, "_wst") or self._wst
+                or any(self._sts[i] for i in range(len(self._sts)))):
             raise XfgStarkError(9, "record_views: call record_ready() first (and it must have succeeded)")
         return [memoryview((C.c_uint8 * self._cap).from_address(self._base + i * self._cap)).cast("B")[:self._lens[i]]
                 for i in range(len(self._sts))]
