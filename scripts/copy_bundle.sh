@@ -1,9 +1,9 @@
 #!/bin/bash
-# CPU container: copy a final-build bundle (scripts/r5_bundle.sh output under gpurun_out/) into
-# profiles/$1 (default r05) under the names profiles/*/INDEX.md cites, and add the VALU ledger's
+# CPU container: copy a final-build bundle (scripts/round_bundle.sh output under gpurun_out/) into
+# profiles/$1 (default r06) under the names profiles/*/INDEX.md cites, and add the VALU ledger's
 # instruction-mix ceiling from this tree's ISA listings
 set -e
-R=${1:-r05}
+R=${1:-r06}
 P=profiles/$R
 G=gpurun_out
 cp $G/round/bench.json $P/bench.json
@@ -19,6 +19,8 @@ done
 cp $G/smoke.txt $P/smoke.txt
 tail -1 $G/bench_default.json > $P/bench_default.json
 cp $G/valu/valu_per_proof.json $P/valu_per_proof.json
+cp $G/single_summary.txt $P/single_proof.txt
+cp $G/single/single_kernel_stats.csv $P/single_kernel_stats.csv
 T=$(mktemp -d /tmp/xfg_isa.XXXX)
 for f in ntt kernels prover; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 --cuda-device-only -S -o $T/$f.s xfg-stark_amd/csrc/$f.hip
