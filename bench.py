@@ -209,6 +209,8 @@ class Exchange:
 
     def _scatter(self, i):
         slot = i % len(self.in_pending)
+        if self.in_pending[slot] is not None:  # the slot's previous scatter (rank 0 took its own shard
+            self._done(self.in_pending[slot][1])  # locally and did not wait for it): long done by now
         chunks = list(self.packed[i].unbind(0)) if self.rank == 0 else None
 
         def job():
@@ -218,14 +220,19 @@ class Exchange:
                 self._copy(self.side, self.in_host[slot], self.in_dev)
         self.in_pending[slot] = (i, self._submit(job))
 
-    def inputs(self, i):
-        """step i's shard as prove kwargs (issues step i + lookahead's scatter)"""
+    def inputs(self, i, local=None):
+        """step i's shard as prove kwargs (issues step i + lookahead's scatter). `local`: the root's own
+        shard, which it holds already (rank 0 proves it without waiting for its chunk of the scatter --
+        the scatter still runs for the peers, as MPI's root keeps its own chunk)"""
         slot = i % len(self.in_pending)
         j, h = self.in_pending[slot]
         assert j == i, (j, i)
-        self._done(h)
-        kws = unpack_inputs(self.in_host[slot].numpy())
-        self.in_pending[slot] = None
+        if local is None:
+            self._done(h)
+            kws = unpack_inputs(self.in_host[slot].numpy())
+            self.in_pending[slot] = None
+        else:
+            kws = local
         if i + self.lookahead < self.nsteps:
             self._scatter(i + self.lookahead)
         return kws
@@ -402,7 +409,7 @@ def pipelined_steps(submit_fn, collect_fn, batches, depth=2, ex=None, packed=Non
         t1 = clk()
         s, rec = None, None
         if ex is not None:
-            b = ex.inputs(i)
+            b = ex.inputs(i, b[:ex.per] if ex.rank == 0 and b is not None else None)
             s, addr, nbytes, owner = ex.claim()
             rec = (addr, nbytes, owner)
         t2 = clk()
