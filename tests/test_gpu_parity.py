@@ -1,8 +1,9 @@
 """GPU parity: libxfgstark.so (HIP, gfx950) against the CPU oracle, bit for bit.
 
 Kernel level: coset LDE / interpolation vs oracle NTT. Proof level: StarkProof bytes of the GPU
-path == oracle bytes on the same ExecutionTrace / burn inputs (small sizes run the oracle live;
-config-2 size n=2^16 is checked against the committed oracle fixture digest). Large sizes beyond
+path == oracle bytes on the same ExecutionTrace / burn inputs (small sizes run the oracle live; the
+benchmark shapes -- configs[2]'s 128 proofs of n=2^16 and the configs[4] proof of n=2^20 x 16,
+quadratic -- are checked against committed oracle digests, tests/golden/). Large sizes beyond
 the fixtures are checked through size-independent properties (the oracle verifier accepts,
 determinism, batch == single)."""
 import hashlib
