@@ -2,6 +2,7 @@
 with the most kernels between idle gaps > 0.5 ms (the warmup drains before the barrier); per 2 ms
 bucket, the fraction of time any kernel runs and the mean number of kernels in flight."""
 import csv
+import os
 import glob
 import sys
 
@@ -58,6 +59,6 @@ if m:
     h0, h1 = int(m.group(1)), int(m.group(2))
     print(f"host window {(h1 - h0) / 1e6:.2f} ms: first kernel {(t0 - h0) / 1e6:+.2f} ms after its start, "
           f"last kernel end {(h1 - t1) / 1e6:.2f} ms before its end")
-    tail = sorted(win, key=lambda x: x[1])[-12:]
+    tail = sorted(win, key=lambda x: x[1])[-int(os.environ.get("TAIL", "12")):]
     for s_, e_, n_ in tail:
         print(f"  {(s_ - h0) / 1e6:8.2f} {(e_ - h0) / 1e6:8.2f}  {n_[:80]}")
