@@ -24,7 +24,8 @@ def run(reps, calls_path):
     pr = xfgstark.XfgBurnMintProver()
     n = 1 << 16
     kw = synthetic.burn_inputs(0)
-    pr.prove_burn_mint(**kw, trace_length=n)  # warm: workspace, code objects
+    pr.prepare(1, n)  # every lane's workspace and code objects, as bench.py does before its timing
+    pr.prove_burn_mint(**kw, trace_length=n)  # warm
     spans = []
     for _ in range(reps):
         t0 = time.perf_counter()

@@ -509,6 +509,8 @@ struct HostTrace {
 
 // the lane's stream for the openings' gathers, at the highest stream priority (a second stream at
 // the default priority measured 4-5 % slower)
+// created with the lane (create_lane_streams): a high-priority stream costs ~10 ms to create, which a
+// lazily created one added to the first unit every lane ran (XFG_TRACE, profiles/r06/host_phases.txt)
 static hipStream_t gather_stream(Lane* c) {
     if (!c->gstream) {
         int least = 0, greatest = 0;
@@ -1098,12 +1100,18 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     }
 }
 
+// a lane's streams and events: the proving stream at the default priority (graded or high lane
+// priorities measured equal or worse) and the openings' high-priority gather stream
+static void create_lane_streams(xfg_ctx* c, Lane* L) {
+    L->lde_probe = c->lde_probe;
+    HIPCHK(hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking));
+    for (auto& e : L->ev) HIPCHK(hipEventCreate(&e));
+    gather_stream(L);
+}
 static Lane* lane0(xfg_ctx* c) {
     if (c->lanes.empty()) {
         c->lanes.emplace_back(new Lane());
-        c->lanes[0]->lde_probe = c->lde_probe;
-        HIPCHK(hipStreamCreateWithFlags(&c->lanes[0]->stream, hipStreamNonBlocking));
-        for (auto& e : c->lanes[0]->ev) HIPCHK(hipEventCreate(&e));
+        create_lane_streams(c, c->lanes[0].get());
     }
     return c->lanes[0].get();
 }
@@ -1111,10 +1119,7 @@ static void ensure_lanes(xfg_ctx* c, size_t k) {
     lane0(c);
     while (c->lanes.size() < k) {
         c->lanes.emplace_back(new Lane());
-        c->lanes.back()->lde_probe = c->lde_probe;
-        // every lane at the default priority (graded or high lane priorities measured equal or worse)
-        HIPCHK(hipStreamCreateWithFlags(&c->lanes.back()->stream, hipStreamNonBlocking));
-        for (auto& e : c->lanes.back()->ev) HIPCHK(hipEventCreate(&e));
+        create_lane_streams(c, c->lanes.back().get());
     }
 }
 // lane / work-unit tuning knobs (XFG_LANES, XFG_UNIT)
