@@ -509,8 +509,9 @@ struct HostTrace {
 
 // the lane's stream for the openings' gathers, at the highest stream priority (a second stream at
 // the default priority measured 4-5 % slower)
-// created with the lane (create_lane_streams): a high-priority stream costs ~10 ms to create, which a
-// lazily created one added to the first unit every lane ran (XFG_TRACE, profiles/r06/host_phases.txt)
+// created when the lanes are (ensure_lanes, after every lane's proving stream): a high-priority stream
+// costs ~10 ms to create, which a lazily created one added to the first unit every lane ran (XFG_TRACE,
+// profiles/r06/host_phases.txt); lane 0 used alone (the debug / bench entry points) creates it here
 static hipStream_t gather_stream(Lane* c) {
     if (!c->gstream) {
         int least = 0, greatest = 0;
@@ -1100,27 +1101,31 @@ static void prove_lane(Lane* c, const Tables& T, const u64* ce_div, ProofJob* jo
     }
 }
 
-// a lane's streams and events: the proving stream at the default priority (graded or high lane
-// priorities measured equal or worse) and the openings' high-priority gather stream
-static void create_lane_streams(xfg_ctx* c, Lane* L) {
+// a lane's proving stream (default priority: graded or high lane priorities measured equal or worse)
+// and events
+static void create_lane_stream(xfg_ctx* c, Lane* L) {
     L->lde_probe = c->lde_probe;
     HIPCHK(hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking));
     for (auto& e : L->ev) HIPCHK(hipEventCreate(&e));
-    gather_stream(L);
 }
 static Lane* lane0(xfg_ctx* c) {
     if (c->lanes.empty()) {
         c->lanes.emplace_back(new Lane());
-        create_lane_streams(c, c->lanes[0].get());
+        create_lane_stream(c, c->lanes[0].get());
     }
     return c->lanes[0].get();
 }
+// every lane's proving stream first, then the gather streams: streams take the process's hardware
+// queues (GPU_MAX_HW_QUEUES, 4) in creation order, and a gather stream created between two lanes'
+// proving streams left the proving streams two of the four queues (-9 % burn-proofs/s,
+// profiles/r06/gather_stream_ab.txt)
 static void ensure_lanes(xfg_ctx* c, size_t k) {
     lane0(c);
     while (c->lanes.size() < k) {
         c->lanes.emplace_back(new Lane());
-        create_lane_streams(c, c->lanes.back().get());
+        create_lane_stream(c, c->lanes.back().get());
     }
+    for (auto& L : c->lanes) gather_stream(L.get());
 }
 // lane / work-unit tuning knobs (XFG_LANES, XFG_UNIT)
 static int env_int(const char* name, int dflt) {
