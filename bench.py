@@ -753,6 +753,60 @@ def rank_cpus(local_rank, local_world, cpus):
     return cpus[local_rank * k:(local_rank + 1) * k]
 
 
+def parse_cpulist(text):
+    """sysfs cpulist ("0-63,128-191") -> set of CPU ids"""
+    out = set()
+    for part in text.strip().split(","):
+        if part:
+            a, _, b = part.partition("-")
+            out.update(range(int(a), int(b or a) + 1))
+    return out
+
+
+def gpu_local_cpus(index, sysfs="/sys", env=None):
+    """the CPUs local to GPU `index` of this process's device order: the index-th GPU node of the KFD
+    topology (the order HIP enumerates devices in, modulo the device count: ranks sharing a GPU in a
+    rehearsal) -> its PCI device's local_cpulist. None when the topology is not readable, or when a
+    *_VISIBLE_DEVICES variable renumbers the devices (then the order cannot be read from sysfs)"""
+    env = os.environ if env is None else env
+    if any(env.get(v) for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES",
+                                 "GPU_DEVICE_ORDINAL")):
+        return None
+    base = os.path.join(sysfs, "class", "kfd", "kfd", "topology", "nodes")
+    try:
+        gpus = []
+        for d in sorted(os.listdir(base), key=int):
+            with open(os.path.join(base, d, "properties")) as f:
+                props = dict(ln.split()[:2] for ln in f if len(ln.split()) >= 2)
+            if int(props.get("simd_count", "0")) > 0:
+                gpus.append(props)
+        p = gpus[index % len(gpus)]
+        loc, dom = int(p["location_id"]), int(p.get("domain", "0"))
+        bdf = f"{dom:04x}:{loc >> 8:02x}:{(loc >> 3) & 31:02x}.{loc & 7:x}"
+        with open(os.path.join(sysfs, "bus", "pci", "devices", bdf, "local_cpulist")) as f:
+            return parse_cpulist(f.read()) or None
+    except (OSError, ValueError, KeyError, ZeroDivisionError):
+        return None
+
+
+def rank_cpus_local(local_rank, local_world, cpus, local_sets):
+    """NUMA-aware rank_cpus: the ranks whose GPUs share a set of local CPUs split that set (within the
+    CPUs this process may use) between them, so every rank's host threads -- which fill the pinned
+    host blocks its GPU reads and writes directly -- sit next to its GPU; rank_cpus when any rank's
+    local set is unknown or too small for the ranks that share it"""
+    cpus = set(cpus)
+    if local_world <= 1 or any(ls is None for ls in local_sets):
+        return rank_cpus(local_rank, local_world, cpus)
+    mine = local_sets[local_rank]
+    peers = [r for r in range(local_world) if local_sets[r] == mine]
+    pool = sorted(mine & cpus)
+    k = len(pool) // len(peers)
+    if k == 0:
+        return rank_cpus(local_rank, local_world, cpus)
+    i = peers.index(local_rank)
+    return pool[i * k:(i + 1) * k]
+
+
 def host_threads_for(ncpus):
     """XFG_HOST_THREADS for a rank with `ncpus` CPUs: the library's default 8 on a 16-CPU share (the
     other half runs the lane workers), fewer on a smaller share"""
@@ -760,13 +814,19 @@ def host_threads_for(ncpus):
 
 
 def pin_rank(env):
-    """pin this rank (before torch or HIP start any thread) to its slice of the node's CPUs and size
-    the library's host pool to it, unless the caller set XFG_HOST_THREADS; -> the slice"""
+    """pin this rank (before torch or HIP start any thread) to its slice of the node's CPUs -- next to
+    its GPU where the topology says which CPUs those are -- and size the library's host pool to it,
+    unless the caller set XFG_HOST_THREADS; -> the slice"""
     if not hasattr(os, "sched_setaffinity"):
         return None
     local_world = int(env.get("LOCAL_WORLD_SIZE", env.get("WORLD_SIZE", "1")))
-    mine = rank_cpus(int(env.get("LOCAL_RANK", "0")), local_world, os.sched_getaffinity(0))
+    local_rank = int(env.get("LOCAL_RANK", "0"))
+    cpus = os.sched_getaffinity(0)
+    mine = sorted(cpus)
     if local_world > 1:
+        # NUMA-aware when the GPU topology is readable: on a two-socket node a contiguous slice by CPU
+        # id would put half the ranks on the socket away from their GPU
+        mine = rank_cpus_local(local_rank, local_world, cpus, [gpu_local_cpus(r, env=env) for r in range(local_world)])
         os.sched_setaffinity(0, mine)
         env.setdefault("XFG_HOST_THREADS", str(host_threads_for(len(mine))))
     return mine

@@ -413,6 +413,50 @@ def test_rank_cpu_slices():
     assert [bench.host_threads_for(k) for k in (1, 2, 4, 16, 32)] == [2, 2, 2, 8, 8]
 
 
+def _fake_sysfs(root, gpus):
+    """a KFD topology with one CPU node and `gpus` = [(pci bus, local_cpulist)] GPU nodes"""
+    nodes = root / "class" / "kfd" / "kfd" / "topology" / "nodes"
+    (nodes / "0").mkdir(parents=True)
+    (nodes / "0" / "properties").write_text("cpu_cores_count 128\nsimd_count 0\n")
+    for i, (bus, cl) in enumerate(gpus):
+        d = nodes / str(i + 1)
+        d.mkdir()
+        (d / "properties").write_text(f"cpu_cores_count 0\nsimd_count 1024\nlocation_id {bus << 8}\ndomain 0\n")
+        dev = root / "bus" / "pci" / "devices" / f"0000:{bus:02x}:00.0"
+        dev.mkdir(parents=True)
+        (dev / "local_cpulist").write_text(cl + "\n")
+
+
+def test_rank_cpu_slices_numa(tmp_path):
+    """on a two-socket node (GPUs 0-3 next to CPUs 0-63,128-191, GPUs 4-7 next to 64-127,192-255),
+    every rank's slice lies in its own GPU's local set, the slices are disjoint, and each takes a
+    quarter of its socket; a renumbering *_VISIBLE_DEVICES or a missing topology falls back to the
+    contiguous split"""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    s0, s1 = "0-63,128-191", "64-127,192-255"
+    _fake_sysfs(tmp_path, [(0x10 + 0x10 * g, s0 if g < 4 else s1) for g in range(8)])
+    assert bench.parse_cpulist(s0) == set(range(64)) | set(range(128, 192))
+    env = {}
+    local = [bench.gpu_local_cpus(r, sysfs=str(tmp_path), env=env) for r in range(8)]
+    assert local[0] == bench.parse_cpulist(s0) and local[7] == bench.parse_cpulist(s1)
+    sl = [bench.rank_cpus_local(r, 8, range(256), local) for r in range(8)]
+    assert all(len(x) == 32 and set(x) <= local[r] for r, x in enumerate(sl))
+    assert len(set().union(*map(set, sl))) == 256
+    # the contiguous split would have put ranks 2, 3 on the other socket
+    assert not set(bench.rank_cpus(2, 8, range(256))) <= local[2]
+    assert bench.gpu_local_cpus(0, sysfs=str(tmp_path), env={"HIP_VISIBLE_DEVICES": "1"}) is None
+    assert bench.gpu_local_cpus(0, sysfs=str(tmp_path / "none"), env=env) is None
+    assert bench.rank_cpus_local(1, 2, range(8), [None, {0, 1}]) == bench.rank_cpus(1, 2, range(8))
+    # ranks sharing one GPU (the one-GPU rehearsals): its local set split between them
+    one = tmp_path / "one"
+    _fake_sysfs(one, [(0x10, "0-15")])
+    loc = [bench.gpu_local_cpus(r, sysfs=str(one), env=env) for r in range(2)]
+    assert [bench.rank_cpus_local(r, 2, range(64), loc) for r in range(2)] == [list(range(8)), list(range(8, 16))]
+
+
 def test_bench_gpus_mismatch_fails_loudly():
     """under a launcher, --gpus must equal WORLD_SIZE: a mismatch exits non-zero before any GPU work
     instead of printing a line for a different N"""
