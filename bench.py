@@ -764,28 +764,32 @@ def parse_cpulist(text):
 
 
 def gpu_local_cpus(index, sysfs="/sys", env=None):
-    """the CPUs local to GPU `index` of this process's device order: the index-th GPU node of the KFD
-    topology (the order HIP enumerates devices in, modulo the device count: ranks sharing a GPU in a
-    rehearsal) -> its PCI device's local_cpulist. None when the topology is not readable, or when a
-    *_VISIBLE_DEVICES variable renumbers the devices (then the order cannot be read from sysfs)"""
+    """the CPUs local to GPU `index` of this process's device order: the GPU nodes of the KFD topology
+    this process may open, in topology order (the order ROCr enumerates them), narrowed by
+    ROCR_VISIBLE_DEVICES and then HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES (index lists into the
+    previous list), modulo the count (ranks sharing a GPU in a rehearsal) -> that PCI device's
+    local_cpulist. None when the topology is not readable or a visibility list is not plain indices"""
     env = os.environ if env is None else env
-    if any(env.get(v) for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES",
-                                 "GPU_DEVICE_ORDINAL")):
-        return None
     base = os.path.join(sysfs, "class", "kfd", "kfd", "topology", "nodes")
     try:
         gpus = []
         for d in sorted(os.listdir(base), key=int):
-            with open(os.path.join(base, d, "properties")) as f:
-                props = dict(ln.split()[:2] for ln in f if len(ln.split()) >= 2)
+            try:  # a GPU this process may not open (a shared box's other cards) is not one of its devices
+                with open(os.path.join(base, d, "properties")) as f:
+                    props = dict(ln.split()[:2] for ln in f if len(ln.split()) >= 2)
+            except PermissionError:
+                continue
             if int(props.get("simd_count", "0")) > 0:
                 gpus.append(props)
+        for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+            if env.get(var):
+                gpus = [gpus[int(i)] for i in env[var].split(",")]
         p = gpus[index % len(gpus)]
         loc, dom = int(p["location_id"]), int(p.get("domain", "0"))
         bdf = f"{dom:04x}:{loc >> 8:02x}:{(loc >> 3) & 31:02x}.{loc & 7:x}"
         with open(os.path.join(sysfs, "bus", "pci", "devices", bdf, "local_cpulist")) as f:
             return parse_cpulist(f.read()) or None
-    except (OSError, ValueError, KeyError, ZeroDivisionError):
+    except (OSError, ValueError, KeyError, IndexError, ZeroDivisionError):
         return None
 
 

@@ -430,8 +430,8 @@ def _fake_sysfs(root, gpus):
 def test_rank_cpu_slices_numa(tmp_path):
     """on a two-socket node (GPUs 0-3 next to CPUs 0-63,128-191, GPUs 4-7 next to 64-127,192-255),
     every rank's slice lies in its own GPU's local set, the slices are disjoint, and each takes a
-    quarter of its socket; a renumbering *_VISIBLE_DEVICES or a missing topology falls back to the
-    contiguous split"""
+    quarter of its socket; *_VISIBLE_DEVICES lists are followed; a missing topology or a non-index
+    visibility list falls back to the contiguous split"""
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, root)
@@ -447,9 +447,20 @@ def test_rank_cpu_slices_numa(tmp_path):
     assert len(set().union(*map(set, sl))) == 256
     # the contiguous split would have put ranks 2, 3 on the other socket
     assert not set(bench.rank_cpus(2, 8, range(256))) <= local[2]
-    assert bench.gpu_local_cpus(0, sysfs=str(tmp_path), env={"HIP_VISIBLE_DEVICES": "1"}) is None
+    # visibility lists index into the previous list: ROCr's, then HIP's
+    vis = {"ROCR_VISIBLE_DEVICES": "6,2,5", "HIP_VISIBLE_DEVICES": "2,1"}
+    assert [bench.gpu_local_cpus(r, sysfs=str(tmp_path), env=vis) for r in range(2)] == [local[5], local[2]]
+    assert bench.gpu_local_cpus(0, sysfs=str(tmp_path), env={"HIP_VISIBLE_DEVICES": "GPU-1234"}) is None
+    assert bench.gpu_local_cpus(0, sysfs=str(tmp_path), env={"ROCR_VISIBLE_DEVICES": "9"}) is None
     assert bench.gpu_local_cpus(0, sysfs=str(tmp_path / "none"), env=env) is None
     assert bench.rank_cpus_local(1, 2, range(8), [None, {0, 1}]) == bench.rank_cpus(1, 2, range(8))
+    # a node whose other cards this process may not open: only the readable GPU node counts
+    part = tmp_path / "part"
+    _fake_sysfs(part, [(0x10, s0), (0x20, s1)])
+    prop = part / "class" / "kfd" / "kfd" / "topology" / "nodes" / "1" / "properties"
+    prop.chmod(0)
+    if os.geteuid() != 0:  # root reads mode-0 files anyway
+        assert bench.gpu_local_cpus(0, sysfs=str(part), env=env) == bench.parse_cpulist(s1)
     # ranks sharing one GPU (the one-GPU rehearsals): its local set split between them
     one = tmp_path / "one"
     _fake_sysfs(one, [(0x10, "0-15")])
