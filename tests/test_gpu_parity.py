@@ -69,7 +69,7 @@ def test_lde_kernel_tile_paths_match_oracle(prover, n, blowup):
     assert np.array_equal(got, O.evaluate_lde_np(coef[0], blowup, 7))
 
 
-@pytest.mark.parametrize("npoly,blowup", [(32, 8), (32, 2), (33, 16), (28, 8)])
+@pytest.mark.parametrize("npoly,blowup", [(32, 8), (32, 2), (32, 4), (33, 16), (28, 8)])
 def test_lde_launch_set_routes_match_oracle(prover, npoly, blowup):
     """the two routes of the tabled 2^16 forward LDE: launch sets of >= 512 all-coset blocks (16 per
     polynomial: 32 or 33 polynomials) take ntt_pass_a_cos2 (beta >= 4) / ntt_pass_a_cos (beta = 2) +
