@@ -186,7 +186,8 @@ int xfg_debug_interpolate(xfg_ctx* ctx, const uint64_t* evals, uint32_t npoly, u
 /* Goldilocks primitive self test on the device: out[i] = op(a[i], b[i]) with op 0 mul, 1 add,
  * 2 sub, 3 canonical(a), 4 a * 2^(b mod 96), 5 a + (b mod 2^32) * (2^32 - 1), 6 a - b with one
  * borrow fold (the weak subtraction of the NTT butterflies), 7 a + b with one carry fold (the weak
- * addition of the NTT butterflies, b < p) */
+ * addition of the NTT butterflies, b < p), 8 a * b through the interleaved pair multiply (gl_mul2:
+ * both a * b and b * a computed, all ones returned if they differ) */
 int xfg_debug_field(xfg_ctx* ctx, uint32_t op, uint64_t count, const uint64_t* a, const uint64_t* b, uint64_t* out);
 /* OOD evaluation + DEEP quotient kernels of the prover on `count` instances: coef [count][7][n],
  * hcoef [count][n] (trace / composition coefficients), zpts [count][2] = (z, z g), coeffs

@@ -116,7 +116,7 @@ def _field_inputs(canonical, seed):
     return a, b
 
 
-@pytest.mark.parametrize("op", ["mul", "add", "sub", "canon", "pow2", "fold", "sub_weak", "add_w"])
+@pytest.mark.parametrize("op", ["mul", "add", "sub", "canon", "pow2", "fold", "sub_weak", "add_w", "mul2"])
 def test_field_primitives_match_bigint(prover, op):
     """the gfx950 inline-asm Goldilocks primitives (gl.hpp) against Python integers, edge values
     (0, 2^32 - 1, p - 1, p, 2^64 - 1, ...) crossed with each other plus random operands"""
@@ -130,7 +130,7 @@ def test_field_primitives_match_bigint(prover, op):
         b = [y % P_GL for y in b]
     got = prover.debug_field(op, np.array(a, dtype=np.uint64), np.array(b, dtype=np.uint64)).tolist()
     for x, y, r in zip(a, b, got):
-        if op == "mul":
+        if op in ("mul", "mul2"):  # mul2: the interleaved pair (x y, y x), both checked on the device
             want = x * y % P_GL
         elif op == "add":
             want = (x + y) % P_GL

@@ -197,6 +197,61 @@ __host__ __device__ __forceinline__ u64 gl_mul(u64 a, u64 b) {
     return gl_reduce(mulhi64(a, b), a * b);
 #endif
 }
+// two independent products a * b, c * d with their instruction streams interleaved: each one's
+// carry / borrow wait states are filled by the other's instructions (3 s_nop 0 for the pair instead of
+// 4 s_nop 1 each); results identical to gl_mul
+__host__ __device__ __forceinline__ void gl_mul2(u64& a, u64 b, u64& c, u64 d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    u64 pA, t1A, t2A, hiA, xA, sA, cA, pB, t1B, t2B, hiB, xB, sB, cB;
+    const u32 a0 = (u32)a, a1 = (u32)(a >> 32), b0 = (u32)b, b1 = (u32)(b >> 32);
+    const u32 c0 = (u32)c, c1 = (u32)(c >> 32), d0 = (u32)d, d1 = (u32)(d >> 32);
+    asm("v_mad_u64_u32 %[pA], %[sA], %[a0], %[b0], 0\n\t"
+        "v_mad_u64_u32 %[pB], %[sB], %[c0], %[d0], 0\n\t"
+        "v_lshrrev_b64 %[xA], 32, %[pA]\n\t"
+        "v_lshrrev_b64 %[xB], 32, %[pB]\n\t"
+        "v_mad_u64_u32 %[t1A], %[sA], %[a0], %[b1], %[xA]\n\t"
+        "v_mad_u64_u32 %[t1B], %[sB], %[c0], %[d1], %[xB]\n\t"
+        "v_mad_u64_u32 %[t2A], %[cA], %[a1], %[b0], %[t1A]\n\t"
+        "v_mad_u64_u32 %[t2B], %[cB], %[c1], %[d0], %[t1B]\n\t"
+        "v_lshrrev_b64 %[xA], 32, %[t2A]\n\t"
+        "v_lshrrev_b64 %[xB], 32, %[t2B]\n\t"
+        "v_mad_u64_u32 %[hiA], %[sA], %[a1], %[b1], %[xA]\n\t"
+        "v_mad_u64_u32 %[hiB], %[sB], %[c1], %[d1], %[xB]"
+        : [pA] "=&v"(pA), [xA] "=&v"(xA), [t1A] "=&v"(t1A), [t2A] "=&v"(t2A), [hiA] "=&v"(hiA), [sA] "=&s"(sA),
+          [cA] "=&s"(cA), [pB] "=&v"(pB), [xB] "=&v"(xB), [t1B] "=&v"(t1B), [t2B] "=&v"(t2B), [hiB] "=&v"(hiB),
+          [sB] "=&s"(sB), [cB] "=&s"(cB)
+        : [a0] "v"(a0), [a1] "v"(a1), [b0] "v"(b0), [b1] "v"(b1), [c0] "v"(c0), [c1] "v"(c1), [d0] "v"(d0),
+          [d1] "v"(d1));
+    u32 dA0, dA1, mA, eA0, eA1, dB0, dB1, mB, eB0, eB1;
+    u64 bbA, bb2A, bbB, bb2B;
+    // every VALU-written mask is read >= 2 wait states later (the other product's instruction or an s_nop 0
+    // in between); cA / cB were written 4+ instructions before the statement ends
+    asm("s_nop 1\n\t"
+        "v_subb_co_u32_e64 %[dA0], %[bbA], %[lA0], %[hhA], %[cA]\n\t"
+        "v_subb_co_u32_e64 %[dB0], %[bbB], %[lB0], %[hhB], %[cB]\n\t"
+        "s_nop 0\n\t"
+        "v_subb_co_u32_e64 %[dA1], %[bbA], %[lA1], 0, %[bbA]\n\t"
+        "v_subb_co_u32_e64 %[dB1], %[bbB], %[lB1], 0, %[bbB]\n\t"
+        "s_nop 0\n\t"
+        "v_cndmask_b32_e64 %[mA], 0, -1, %[bbA]\n\t"
+        "v_cndmask_b32_e64 %[mB], 0, -1, %[bbB]\n\t"
+        "v_sub_co_u32_e64 %[eA0], %[bb2A], %[dA0], %[mA]\n\t"
+        "v_sub_co_u32_e64 %[eB0], %[bb2B], %[dB0], %[mB]\n\t"
+        "s_nop 0\n\t"
+        "v_subb_co_u32_e64 %[eA1], %[bb2A], %[dA1], 0, %[bb2A]\n\t"
+        "v_subb_co_u32_e64 %[eB1], %[bb2B], %[dB1], 0, %[bb2B]"
+        : [dA0] "=&v"(dA0), [dA1] "=&v"(dA1), [mA] "=&v"(mA), [eA0] "=&v"(eA0), [eA1] "=&v"(eA1), [bbA] "=&s"(bbA),
+          [bb2A] "=&s"(bb2A), [dB0] "=&v"(dB0), [dB1] "=&v"(dB1), [mB] "=&v"(mB), [eB0] "=&v"(eB0), [eB1] "=&v"(eB1),
+          [bbB] "=&s"(bbB), [bb2B] "=&s"(bb2B)
+        : [lA0] "v"((u32)pA), [lA1] "v"((u32)t2A), [hhA] "v"((u32)(hiA >> 32)), [cA] "s"(cA), [lB0] "v"((u32)pB),
+          [lB1] "v"((u32)t2B), [hhB] "v"((u32)(hiB >> 32)), [cB] "s"(cB));
+    a = gl_fold(((u64)eA1 << 32) | eA0, (u32)hiA);
+    c = gl_fold(((u64)eB1 << 32) | eB0, (u32)hiB);
+#else
+    a = gl_mul(a, b);
+    c = gl_mul(c, d);
+#endif
+}
 __host__ __device__ __forceinline__ u64 gl_sqr(u64 a) { return gl_mul(a, a); }
 __host__ __device__ inline u64 gl_pow(u64 b, u64 e) {
     u64 r = 1;

@@ -160,8 +160,12 @@ __device__ __forceinline__ void stockham(int lognseq, int Ns, const u64* ltw, LD
         for (int r = 0; r < R; r++) v[q][r] = ld(seq, j, r * G);
         if (Ns > 1) {
             const int k = j % Ns, step = S / (Ns * R);
+            // in pairs (gl_mul2: each product's carry wait states filled by the other's instructions)
 #pragma unroll
-            for (int r = 1; r < R; r++) v[q][r] = gl_mul(v[q][r], TW2D ? ltw[r * Ns + k] : ltw[r * k * step]);
+            for (int r = 1; r + 1 < R; r += 2)
+                gl_mul2(v[q][r], TW2D ? ltw[r * Ns + k] : ltw[r * k * step], v[q][r + 1],
+                        TW2D ? ltw[(r + 1) * Ns + k] : ltw[(r + 1) * k * step]);
+            v[q][R - 1] = gl_mul(v[q][R - 1], TW2D ? ltw[(R - 1) * Ns + k] : ltw[(R - 1) * k * step]);
         }
         dft_reg<LOGR, INV, CANON_OUT>(v[q]);
         gs[q] = g0 < groups ? seq : -1;
@@ -620,8 +624,11 @@ __global__ __launch_bounds__(256, 3) void ntt_pass_a_r1024(NttArgs a) {
     const auto rt = buf_rsrc(t4 + col0);
     auto stg = [&](int, int seq, int base, int stride, u64* v) {
         const u32 vt = (((u32)base << 10) + seq) * 8;
+        u64 tb[RR];
 #pragma unroll
-        for (int r = 0; r < RR; r++) v[r] = gl_mul(v[r], buf_ld(rt, vt, ((u32)(r * stride) << 10) * 8));
+        for (int r = 0; r < RR; r++) tb[r] = buf_ld(rt, vt, ((u32)(r * stride) << 10) * 8);
+#pragma unroll
+        for (int r = 0; r < RR; r += 2) gl_mul2(v[r], tb[r], v[r + 1], tb[r + 1]);
         store_pairs_buf<RR>(v, ry, (((u32)base << 3) + (seq & ~1)) * 8, ((u32)stride << 3) * 8);
     };
     pass_dft_split<LOGR, LOGE, false, true, NT, decltype(ldg), decltype(stg), NoPf, true>(tile, logTC, comb, ldg, stg,
@@ -1195,6 +1202,12 @@ __global__ void field_op_kernel(int op, const u64* a, const u64* b, u64* out, u6
         case 5: r = gl_fold(x, (u32)y); break;
         case 6: r = gl_sub_weak(x, y); break;
         case 7: r = add_w(x, y); break;
+        case 8: {  // gl_mul2: both products (x y and y x) must equal; the first is returned
+            u64 p = x, q = y;
+            gl_mul2(p, y, q, x);
+            r = p == q ? p : ~0ULL;
+            break;
+        }
         default: break;
     }
     out[i] = r;

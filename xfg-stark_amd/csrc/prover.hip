@@ -1793,7 +1793,7 @@ int xfg_debug_interpolate(xfg_ctx* c, const uint64_t* evals, uint32_t npoly, uin
 }
 
 int xfg_debug_field(xfg_ctx* c, uint32_t op, uint64_t count, const uint64_t* a, const uint64_t* b, uint64_t* out) {
-    if (!c || !a || !b || !out || op > 7 || count == 0) return XFG_INVALID_ARGUMENT;
+    if (!c || !a || !b || !out || op > 8 || count == 0) return XFG_INVALID_ARGUMENT;
     if (busy(c)) {
         c->err = "batches pending: call xfg_batch_wait first";
         return XFG_INVALID_ARGUMENT;

@@ -694,7 +694,7 @@ class XfgBurnMintProver:
             raise self._err(st)
         return ood, deep
 
-    FIELD_OPS = {"mul": 0, "add": 1, "sub": 2, "canon": 3, "pow2": 4, "fold": 5, "sub_weak": 6, "add_w": 7}
+    FIELD_OPS = {"mul": 0, "add": 1, "sub": 2, "canon": 3, "pow2": 4, "fold": 5, "sub_weak": 6, "add_w": 7, "mul2": 8}
 
     def debug_field(self, op, a, b):
         """device Goldilocks primitive `op` (FIELD_OPS) applied elementwise to u64 arrays a, b"""
