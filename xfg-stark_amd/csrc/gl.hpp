@@ -274,9 +274,14 @@ struct E2 {
 __host__ __device__ __forceinline__ E2 e2(u64 a, u64 b = 0) { return E2{a, b}; }
 __host__ __device__ __forceinline__ E2 e2_add(E2 x, E2 y) { return E2{gl_add(x.a, y.a), gl_add(x.b, y.b)}; }
 __host__ __device__ __forceinline__ E2 e2_sub(E2 x, E2 y) { return E2{gl_sub(x.a, y.a), gl_sub(x.b, y.b)}; }
-__host__ __device__ __forceinline__ E2 e2_mulb(E2 x, u64 s) { return E2{gl_mul(x.a, s), gl_mul(x.b, s)}; }
+// (the coordinate products in pairs through gl_mul2)
+__host__ __device__ __forceinline__ E2 e2_mulb(E2 x, u64 s) {
+    gl_mul2(x.a, s, x.b, s);
+    return x;
+}
 __host__ __device__ __forceinline__ E2 e2_mul(E2 x, E2 y) {
-    const u64 a0b0 = gl_mul(x.a, y.a), a1b1 = gl_mul(x.b, y.b);
+    u64 a0b0 = x.a, a1b1 = x.b;
+    gl_mul2(a0b0, y.a, a1b1, y.b);
     const u64 m = gl_mul(gl_add(x.a, x.b), gl_add(y.a, y.b));
     return E2{gl_sub(a0b0, gl_add(a1b1, a1b1)), gl_sub(m, a0b0)};
 }
@@ -321,7 +326,10 @@ __host__ __device__ __forceinline__ FE<1> fe_mul(FE<1> x, FE<1> y) { return FE<1
 __host__ __device__ __forceinline__ FE<1> fe_mulb(FE<1> x, u64 s) { return FE<1>{gl_mul(x.a, s)}; }
 __host__ __device__ __forceinline__ FE<2> fe_add(FE<2> x, FE<2> y) { return FE<2>{gl_add(x.a, y.a), gl_add(x.b, y.b)}; }
 __host__ __device__ __forceinline__ FE<2> fe_sub(FE<2> x, FE<2> y) { return FE<2>{gl_sub(x.a, y.a), gl_sub(x.b, y.b)}; }
-__host__ __device__ __forceinline__ FE<2> fe_mulb(FE<2> x, u64 s) { return FE<2>{gl_mul(x.a, s), gl_mul(x.b, s)}; }
+__host__ __device__ __forceinline__ FE<2> fe_mulb(FE<2> x, u64 s) {
+    gl_mul2(x.a, s, x.b, s);
+    return x;
+}
 __host__ __device__ __forceinline__ FE<2> fe_mul(FE<2> x, FE<2> y) {
     E2 r = e2_mul(E2{x.a, x.b}, E2{y.a, y.b});
     return FE<2>{r.a, r.b};
