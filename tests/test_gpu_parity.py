@@ -471,6 +471,29 @@ def test_config5_quadratic_2p20_blowup16(prover):
     assert prover.prove_burn_mint(**kw, trace_length=1 << 20).to_bytes() == p1
 
 
+@pytest.mark.parametrize("shape", ["config5", "config2"])
+def test_repeated_single_proofs_identical(prover, shape):
+    """The same proof requested 16 times in a row, one synchronous call each: the calls land on
+    different lanes, some of them fresh, so any race or unmodelled hazard in the kernels (a result that
+    depends on timing) shows up as a proof whose bytes differ. Every one must equal the committed oracle
+    digest (configs[4] at n = 2^20, and configs[2]'s first proof at 2^16). A round-6 butterfly variant
+    (two borrow chains in one asm block) returned a different trace, composition or FRI root in about 1
+    of 4 such configs[4] proofs while every single-call test passed (profiles/r06/determinism.txt)"""
+    import xfgstark
+    o = xfgstark.ProofOptions.reference()
+    if shape == "config5":
+        gold = _config_golden("config5")
+        o.field_extension, o.blowup_factor, o.num_queries = 2, 16, 24
+        src, n, want = gold["source"], gold["n"], gold["sha256"]
+    else:
+        gold = _config_golden("config2_batch")
+        src, n, want = 0, gold["n"], gold["proofs"][0]["sha256"]
+    prover._options = o
+    kw = synthetic.burn_inputs(src)
+    got = [hashlib.sha256(prover.prove_burn_mint(**kw, trace_length=n).to_bytes()).hexdigest() for _ in range(16)]
+    assert [i for i, h in enumerate(got) if h != want] == []
+
+
 @pytest.mark.parametrize("ext,n,blowup", [(1, 1024, 8), (2, 512, 16), (1, 1 << 16, 8)])
 def test_gpu_batch_verify_matches_host_verifier(prover, ext, n, blowup):
     """xfg_verify_batch_gpu: same verdicts as the host verifier on GPU-made proofs, valid and

@@ -91,33 +91,6 @@ __device__ __forceinline__ u64 add_w(u64 a, u64 b) {  // b < p
     return s + (u64)c * EPS;
 }
 __device__ __forceinline__ u64 sub_w(u64 a, u64 b) { return gl_sub_weak(a, b); }  // b < p
-// two independent sub_w's with their borrow chains interleaved in one asm block: the compiler lowers
-// each through VCC, so it cannot overlap two of them, and pads every borrow hand-off with s_nop 1;
-// here each chain's borrow lives in its own SGPR pair and the other chain's instructions fill the
-// wait states (10 VALU + 3 s_nop 0 for the pair instead of 10 VALU + 6 s_nop 1). Same results.
-__device__ __forceinline__ void sub_w2(u64 a, u64 b, u64 c, u64 d, u64& x, u64& y) {
-    u32 dlA, dhA, mA, elA, ehA, dlB, dhB, mB, elB, ehB;
-    u64 cA, cB;
-    asm("v_sub_co_u32_e64 %[dlA], %[cA], %[alA], %[blA]\n\t"
-        "v_sub_co_u32_e64 %[dlB], %[cB], %[alB], %[blB]\n\t"
-        "s_nop 0\n\t"
-        "v_subb_co_u32_e64 %[dhA], %[cA], %[ahA], %[bhA], %[cA]\n\t"
-        "v_subb_co_u32_e64 %[dhB], %[cB], %[ahB], %[bhB], %[cB]\n\t"
-        "s_nop 0\n\t"
-        "v_cndmask_b32_e64 %[mA], 0, -1, %[cA]\n\t"
-        "v_cndmask_b32_e64 %[mB], 0, -1, %[cB]\n\t"
-        "v_sub_co_u32_e64 %[elA], %[cA], %[dlA], %[mA]\n\t"
-        "v_sub_co_u32_e64 %[elB], %[cB], %[dlB], %[mB]\n\t"
-        "s_nop 0\n\t"
-        "v_subbrev_co_u32_e64 %[ehA], %[cA], 0, %[dhA], %[cA]\n\t"
-        "v_subbrev_co_u32_e64 %[ehB], %[cB], 0, %[dhB], %[cB]"
-        : [dlA] "=&v"(dlA), [dhA] "=&v"(dhA), [mA] "=&v"(mA), [elA] "=&v"(elA), [ehA] "=&v"(ehA), [cA] "=&s"(cA),
-          [dlB] "=&v"(dlB), [dhB] "=&v"(dhB), [mB] "=&v"(mB), [elB] "=&v"(elB), [ehB] "=&v"(ehB), [cB] "=&s"(cB)
-        : [alA] "v"((u32)a), [ahA] "v"((u32)(a >> 32)), [blA] "v"((u32)b), [bhA] "v"((u32)(b >> 32)),
-          [alB] "v"((u32)c), [ahB] "v"((u32)(c >> 32)), [blB] "v"((u32)d), [bhB] "v"((u32)(d >> 32)));
-    x = ((u64)ehA << 32) | elA;
-    y = ((u64)ehB << 32) | elB;
-}
 __device__ __forceinline__ u64 canon(u64 x) { return gl_canon(x); }
 
 // in-register DFT of size 2^LOGR (<= 32): v[q] <- sum_r v[r] w_R^(+-rq), natural order in/out.
@@ -134,31 +107,6 @@ __device__ __forceinline__ void dft_reg(u64* v) {
     for (int i = 0; i < R; i++) a[i] = v[brev_c(i, LOGR)];
     static_for<LOGR>([&](auto sc) {
         constexpr int s = decltype(sc)::value, h = 1 << s;
-        if constexpr (!(CANON_OUT && s == LOGR - 1) && R >= 4) {
-            // butterflies in pairs: the two subtractions of a pair through sub_w2 (configs[4] LDE
-            // -1.1 %, the 2^16 one unchanged: profiles/r06/bfly2_ab.txt)
-            static_for<R / 4>([&](auto pc) {
-                constexpr int bA = 2 * decltype(pc)::value, bB = bA + 1;
-                constexpr int posA = bA & (h - 1), iA = ((bA >> s) << (s + 1)) + posA;
-                constexpr int posB = bB & (h - 1), iB = ((bB >> s) << (s + 1)) + posB;
-                constexpr int eA0 = (root_exp2(s + 1) * posA) % 192, eB0 = (root_exp2(s + 1) * posB) % 192;
-                constexpr int eA = (INV && eA0) ? 192 - eA0 : eA0, eB = (INV && eB0) ? 192 - eB0 : eB0;
-                u64 tA, tB;
-                if constexpr (eA % 96 != 0) tA = mul_pow2<eA % 96>(a[iA + h]);
-                else if constexpr (s == 0) tA = a[iA + h];
-                else tA = canon(a[iA + h]);
-                if constexpr (eB % 96 != 0) tB = mul_pow2<eB % 96>(a[iB + h]);
-                else if constexpr (s == 0) tB = a[iB + h];
-                else tB = canon(a[iB + h]);
-                const u64 uA = a[iA], uB = a[iB];
-                u64 dA, dB;
-                sub_w2(uA, tA, uB, tB, dA, dB);
-                const u64 sA = add_w(uA, tA), sB = add_w(uB, tB);
-                if constexpr (eA >= 96) { a[iA] = dA; a[iA + h] = sA; } else { a[iA] = sA; a[iA + h] = dA; }
-                if constexpr (eB >= 96) { a[iB] = dB; a[iB + h] = sB; } else { a[iB] = sB; a[iB + h] = dB; }
-            });
-            return;
-        }
         static_for<R / 2>([&](auto bc) {
             constexpr int b = decltype(bc)::value;
             constexpr int pos = b & (h - 1), i0 = ((b >> s) << (s + 1)) + pos;

@@ -278,16 +278,36 @@ __global__ __launch_bounds__(256) void leaves_row_kernel(const u64* lde, Digest*
     }
 }
 
-// openings: recompute the local subtree heaps of selected rows; entry e = proof << logn | m
+// openings: recompute the local subtree heaps of selected rows; entry e = proof << logn | m. One
+// lane per leaf (coset t of row m, 2^LOGB lanes per entry inside a wave): the leaf, then LOGB
+// merge levels with the right child taken from lane l ^ 2^(k-1) -- 1 + LOGB dependent compressions
+// per entry instead of the 2^(LOGB+1) - 1 one lane ran in sequence (a lone proof waits on them).
+// Every lane of a group merges at every level (no divergence around the shuffles); the lanes with
+// t % 2^k == 0 hold level k's nodes and store them to the local heap (slot 1 = top).
 template <int NC, int LOGB>
 __global__ __launch_bounds__(64) void open_rows_kernel(const u64* lde, const u64* entries, u64 count, Digest* out,
                                                        int logn) {
-    const u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= count) return;
+    const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    const u64 e = g >> LOGB;
+    const int t = (int)(g & ((1 << LOGB) - 1));
+    if (e >= count) return;  // whole groups: count is per entry, groups never straddle a wave
     const u64 n = 1ULL << logn, ent = entries[e];
     const u64 proof = ent >> logn, m = ent & (n - 1);
     const u64* base = lde + proof * NC * (1 << LOGB) * n;
-    lde_subtree<NC, LOGB, LOGB, 0>(base, n, m, out + e * (2 << LOGB));
+    Digest* local = out + e * (2 << LOGB);
+    u64 row[NC];
+#pragma unroll
+    for (int c = 0; c < NC; c++) row[c] = base[((u64)c * (1 << LOGB) + t) * n + m];
+    Digest d = b3_hash_elems<NC>(row);
+    local[(1 << LOGB) + t] = d;
+#pragma unroll
+    for (int k = 1; k <= LOGB; k++) {
+        Digest r;
+#pragma unroll
+        for (int w = 0; w < 8; w++) r.w[w] = __shfl_xor(d.w[w], 1 << (k - 1));
+        d = b3_merge(d, r);
+        if ((t & ((1 << k) - 1)) == 0) local[((1 << LOGB) + t) >> k] = d;
+    }
 }
 
 #define XFG_LOGB_DISPATCH(KERNEL, NC, logbeta, ...)                                            \
@@ -324,7 +344,7 @@ u64 launch_leaves_lde(const u64* lde, int nc, Digest* nodes, u64 node_stride, in
 void launch_open_rows(const u64* lde, int nc, const u64* entries, u64 count, Digest* out, int logn, int logbeta,
                       hipStream_t s) {
     if (!count) return;
-    dim3 g((unsigned)((count + 63) / 64)), b(64);
+    dim3 g((unsigned)(((count << logbeta) + 63) / 64)), b(64);
     if (nc == 7) { XFG_LOGB_DISPATCH(open_rows_kernel, 7, logbeta, g, b, 0, s, lde, entries, count, out, logn) }
     else if (nc == 2) { XFG_LOGB_DISPATCH(open_rows_kernel, 2, logbeta, g, b, 0, s, lde, entries, count, out, logn) }
     else { XFG_LOGB_DISPATCH(open_rows_kernel, 1, logbeta, g, b, 0, s, lde, entries, count, out, logn) }
