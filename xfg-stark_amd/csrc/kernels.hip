@@ -351,22 +351,80 @@ void launch_open_rows(const u64* lde, int nc, const u64* entries, u64 count, Dig
     XFG_CHECK_LAUNCH();
 }
 
-// last levels (count <= 512): one block per tree, LDS; then the transcript step `cs` on the root
-__global__ __launch_bounds__(256) void tree_top_kernel(Digest* nodes_all, u64 node_stride, u64 count, CoinStep cs) {
+// One Merkle parent BLAKE3(l || r) (one 64-byte block: CHUNK_START | CHUNK_END | ROOT, counter 0) computed
+// by the four lanes of a quad: lane q holds column q of the state (s[q], s[4 + q], s[8 + q], s[12 + q]) and
+// all 16 message words. The column half is lane q's G function on its own column; for the diagonal half
+// rows 1-3 rotate by 1, 2, 3 lanes (DPP quad_perm, the compiler's hazard padding) so that lane q holds
+// s[q], s[4 + (q+1)%4], s[8 + (q+2)%4], s[12 + (q+3)%4], and rotate back after it. Each lane picks its
+// G's two message words of the round by a 4-way select. ~330 VALU per lane on the critical path instead of
+// one lane's ~680: the serial top levels of a tree (one compression per level) finish about twice as
+// fast, at four lanes per node. Returns (out[q], out[4 + q]).
+__device__ __forceinline__ uint32_t sel4(bool b0, bool b1, uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
+    return b1 ? (b0 ? x3 : x2) : (b0 ? x1 : x0);
+}
+template <int CTRL>
+__device__ __forceinline__ uint32_t quad_perm(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+}
+constexpr int QP_ROT1 = 0x39, QP_ROT2 = 0x4E, QP_ROT3 = 0x93;  // lane q reads lane (q + k) % 4
+#define XFG_B3_GQ(a, b, c, d, x, y)               \
+    do {                                          \
+        a = b3_add3(a, b, (x));                   \
+        d = b3_rotr(b3_xor(d, a), 16);            \
+        c = b3_add(c, d);                         \
+        b = b3_rotr(b3_xor(b, c), 12);            \
+        a = b3_add3(a, b, (y));                   \
+        d = b3_rotr(b3_xor(d, a), 8);             \
+        c = b3_add(c, d);                         \
+        b = b3_rotr(b3_xor(b, c), 7);             \
+    } while (0)
+__device__ __forceinline__ uint2 b3_merge_quad(uint32_t m[16], int q) {
+    const bool q0 = q & 1, q1 = (q & 2) != 0;
+    uint32_t a = sel4(q0, q1, XFG_B3_IV0, XFG_B3_IV1, XFG_B3_IV2, XFG_B3_IV3);
+    uint32_t b = sel4(q0, q1, XFG_B3_IV4, XFG_B3_IV5, XFG_B3_IV6, XFG_B3_IV7);
+    uint32_t c = a;
+    uint32_t d = sel4(q0, q1, 0u, 0u, 64u, B3_CHUNK_START | B3_CHUNK_END | B3_ROOT);
+#pragma unroll
+    for (int r = 0; r < 7; r++) {
+        XFG_B3_GQ(a, b, c, d, sel4(q0, q1, m[0], m[2], m[4], m[6]), sel4(q0, q1, m[1], m[3], m[5], m[7]));
+        b = quad_perm<QP_ROT1>(b);
+        c = quad_perm<QP_ROT2>(c);
+        d = quad_perm<QP_ROT3>(d);
+        XFG_B3_GQ(a, b, c, d, sel4(q0, q1, m[8], m[10], m[12], m[14]), sel4(q0, q1, m[9], m[11], m[13], m[15]));
+        b = quad_perm<QP_ROT3>(b);
+        c = quad_perm<QP_ROT2>(c);
+        d = quad_perm<QP_ROT1>(d);
+        if (r < 6) XFG_B3_PERMUTE(m);
+    }
+    return make_uint2(a ^ c, b ^ d);
+}
+
+// last levels (count <= 512): one block per tree, four lanes per node (b3_merge_quad), the levels
+// through LDS; then the transcript step `cs` on the root
+__global__ __launch_bounds__(1024) void tree_top_kernel(Digest* nodes_all, u64 node_stride, u64 count, CoinStep cs) {
     __shared__ Digest lds[256];
     Digest* nodes = nodes_all + (u64)blockIdx.x * node_stride;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, i = tid >> 2, q = tid & 3;
     for (u64 c = count; c > 1; c >>= 1) {
         const u64 half = c >> 1;
-        Digest d;
-        if (tid < (int)half) {
-            if (c == count) d = b3_merge(nodes[c + 2 * tid], nodes[c + 2 * tid + 1]);
-            else d = b3_merge(lds[2 * tid], lds[2 * tid + 1]);
+        const bool act = i < (int)half;  // whole quads
+        uint2 o = make_uint2(0, 0);
+        if (act) {
+            const Digest* src = c == count ? nodes + c + 2 * i : lds + 2 * i;
+            uint32_t m[16];
+#pragma unroll
+            for (int w = 0; w < 8; w++) {
+                m[w] = src[0].w[w];
+                m[8 + w] = src[1].w[w];
+            }
+            o = b3_merge_quad(m, q);
         }
         __syncthreads();
-        if (tid < (int)half) {
-            lds[tid] = d;
-            nodes[half + tid] = d;
+        if (act) {
+            lds[i].w[q] = o.x;
+            lds[i].w[4 + q] = o.y;
+            nodes[half + i].w[q] = o.x;
+            nodes[half + i].w[4 + q] = o.y;
         }
         __syncthreads();
     }
@@ -392,7 +450,7 @@ void launch_tree_top(Digest* nodes, u64 node_stride, u64 count, int npoly, hipSt
         count /= TREE_MID_SHRINK;
     }
     if (count > 1 || cs.kind != CoinStep::NONE) {
-        int threads = (int)(count / 2);
+        int threads = (int)(2 * count);  // four lanes per node of the widest level
         threads = threads < 64 ? 64 : threads;
         hipLaunchKernelGGL(tree_top_kernel, dim3(npoly), dim3(threads), 0, s, nodes, node_stride, count, cs);
     }
