@@ -755,14 +755,37 @@ __device__ void deep_coin_block(const DeepCoinStep& dc, int b, const u64* o, int
     if (!ok_s || zz) dc.fail[b] = 1;
 }
 // OOD block partials -> the frame ood[proof][15][D]; then the DEEP draws when dc.coins is set
+// The nblk partials of each of the 15 D values are summed by S threads (the most that fit the block), each
+// loading 8 partials before it adds them: one thread per value walking all nblk with a load before
+// each (asm) add waited for every load in turn -- nblk = 32 round trips at 2^16, 512 at 2^20.
 __global__ __launch_bounds__(128) void ood_final_kernel(const u64* partial, int nblk, int d, u64* ood, DeepCoinStep dc) {
     __shared__ u64 o[30];
-    const int proof = blockIdx.x, q = threadIdx.x;
-    if (q < 15 * d) {
+    __shared__ u64 red[8][30];
+    const int proof = blockIdx.x, t = threadIdx.x, nq = 15 * d;
+    int S = 1;
+    while (nq * S * 2 <= (int)blockDim.x && S < 8) S <<= 1;
+    const int q = t % nq, k = t / nq;
+    if (k < S) {
+        const u64* pp = partial + (u64)proof * nblk * nq + q;
         u64 s = 0;
-        for (int b = 0; b < nblk; b++) s = gl_add(s, partial[((u64)proof * nblk + b) * 15 * d + q]);
-        ood[(u64)proof * 15 * d + q] = s;
-        o[q] = s;
+        for (int b0 = k; b0 < nblk; b0 += 8 * S) {
+            u64 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int b = b0 + u * S;
+                v[u] = b < nblk ? pp[(u64)b * nq] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) s = gl_add(s, v[u]);
+        }
+        red[k][q] = s;
+    }
+    __syncthreads();
+    if (t < nq) {
+        u64 s = red[0][t];
+        for (int j = 1; j < S; j++) s = gl_add(s, red[j][t]);
+        ood[(u64)proof * nq + t] = s;
+        o[t] = s;
     }
     if (!dc.coins) return;
     __syncthreads();
