@@ -5,7 +5,7 @@ KAT (src/lib.rs:135-161); they are typed in here as data and checked against the
 produced by it. Proof fixtures ARE produced by the oracle (parity unpinned against real
 Winterfell: see oracle/oracle.h) and pin the restatement against regressions and the GPU path.
 Usage: python tests/golden/make_golden.py            (hash KATs, reference KATs, proofs.json)
-       python tests/golden/make_golden.py --configs  (config_proofs.json: the benchmark shapes, ~10 min
+       python tests/golden/make_golden.py --configs  (config_proofs.json: the benchmark shapes, ~2 min
                                                       on 8 processes)
 """
 import hashlib
@@ -115,6 +115,8 @@ C2_N, C2_COUNT = 1 << 16, 128
 # n = 2^20, blowup 16, quadratic extension, 24 queries, grinding 4, folding 8, remainder 31
 C5_N, C5_SOURCE = 1 << 20, 5005
 C5_OPTIONS = {"blowup": 16, "field_extension": 2, "num_queries": 24}
+# bench.py config5()'s 4-proof batch (synthetic.burn_inputs(50000 + i)), for the pipelined configs[4] test
+C5_BATCH_SOURCES = [50_000 + i for i in range(4)]
 
 
 def _prove_digest(args):
@@ -136,11 +138,14 @@ def config_fixtures(procs=8):
     import multiprocessing as mp
     with mp.get_context("fork").Pool(procs) as pool:
         c5 = pool.apply_async(_prove_digest, ((C5_SOURCE, C5_N, C5_OPTIONS),))
+        c5b = pool.map_async(_prove_digest, [(i, C5_N, C5_OPTIONS) for i in C5_BATCH_SOURCES], chunksize=1)
         c2 = pool.map(_prove_digest, [(i, C2_N, {}) for i in range(C2_COUNT)], chunksize=1)
-        c5 = c5.get()
+        c5, c5b = c5.get(), c5b.get()
     print("config5", c5["len"], c5["sha256"][:16])
+    c5opts = {k: v for k, v in C5_OPTIONS.items() if k != "blowup"}
     return {"config2_batch": {"n": C2_N, "blowup": 8, "options": {}, "proofs": c2},
-            "config5": dict(c5, n=C5_N, blowup=16, options={k: v for k, v in C5_OPTIONS.items() if k != "blowup"})}
+            "config5": dict(c5, n=C5_N, blowup=16, options=c5opts),
+            "config5_batch": {"n": C5_N, "blowup": 16, "options": c5opts, "proofs": c5b}}
 
 
 def main():

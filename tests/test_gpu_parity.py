@@ -471,6 +471,24 @@ def test_config5_quadratic_2p20_blowup16(prover):
     assert prover.prove_burn_mint(**kw, trace_length=1 << 20).to_bytes() == p1
 
 
+def test_config5_pipelined_batches(prover):
+    """bench.py config5()'s own workload: 4-proof configs[4] batches (synthetic.burn_inputs(50000..50003),
+    n = 2^20, blowup 16, quadratic, 24 queries), three calls in flight through submit_batch so that lanes
+    prove them side by side; all 12 proofs equal the committed oracle digests"""
+    import xfgstark
+    gold = _config_golden("config5_batch")
+    assert gold["n"] == 1 << 20 and gold["blowup"] == 16 and gold["options"] == {"field_extension": 2, "num_queries": 24}
+    o = xfgstark.ProofOptions.reference()
+    o.field_extension, o.blowup_factor, o.num_queries = 2, 16, 24
+    prover._options = o
+    kws = [synthetic.burn_inputs(g["source"]) for g in gold["proofs"]]
+    pend = [prover.submit_batch(kws, trace_length=gold["n"]) for _ in range(3)]
+    res = [pb.result() for pb in pend]
+    bad = [(c, i) for c, r in enumerate(res) for i, (p, g) in enumerate(zip(r, gold["proofs"]))
+           if hashlib.sha256(p.to_bytes()).hexdigest() != g["sha256"]]
+    assert bad == [] and all(len(r) == 4 for r in res)
+
+
 @pytest.mark.parametrize("shape", ["config5", "config2"])
 def test_repeated_single_proofs_identical(prover, shape):
     """The same proof requested 16 times in a row, one synchronous call each: the calls land on
