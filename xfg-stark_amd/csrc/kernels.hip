@@ -278,6 +278,43 @@ __global__ __launch_bounds__(256) void leaves_row_kernel(const u64* lde, Digest*
     }
 }
 
+// The same levels for small launch sets (a lone proof: one wave per SIMD, each running the row's
+// 2 beta - 1 compressions in sequence): 2^LOGL lanes per row, each the subtree of beta / 2^LOGL cosets,
+// merged across the lane group (__shfl_xor, every lane of the group merging at every level), then the
+// row-pair level and one more through LDS: 256 / 2^LOGL rows -> a quarter as many nodes per block.
+// 2^LOGL times the waves, and a chain of beta / 2^LOGL + log2 beta + 2 compressions instead of 2 beta + 1.
+constexpr int LEAF_LANES_LOG = 1;  // 2 lanes per row (4: 42.5 + 40.4 against 31.8 + 27.9 µs, profiles/r06/leaves_small_ab.txt)
+template <int LOGB>
+constexpr int leaf_lanes_log() { return LOGB < LEAF_LANES_LOG ? LOGB : LEAF_LANES_LOG; }
+template <int NC, int LOGB>
+__global__ __launch_bounds__(256) void leaves_row2_kernel(const u64* lde, Digest* nodes_all, u64 node_stride,
+                                                          int logn) {
+    constexpr int LOGL = leaf_lanes_log<LOGB>(), RB = 256 >> LOGL;  // lanes per row (log2), rows per block
+    __shared__ Digest lds[RB];
+    const u64 n = 1ULL << logn;
+    const int proof = blockIdx.y, t = threadIdx.x, h = t & ((1 << LOGL) - 1), rl = t >> LOGL;
+    const u64 m = (u64)blockIdx.x * RB + rl;
+    const u64* base = lde + (u64)proof * NC * (1 << LOGB) * n + (u64)h * (1 << (LOGB - LOGL)) * n;
+    Digest d = lde_subtree<NC, LOGB, LOGB - LOGL, 0>(base, n, m, nullptr);
+#pragma unroll
+    for (int k = 0; k < LOGL; k++) {
+        Digest r;
+#pragma unroll
+        for (int w = 0; w < 8; w++) r.w[w] = __shfl_xor(d.w[w], 1 << k);
+        d = (h >> k) & 1 ? b3_merge(r, d) : b3_merge(d, r);
+    }
+    Digest* nodes = nodes_all + (u64)proof * node_stride;
+    if (h == 0) lds[rl] = d;
+    __syncthreads();
+    if (t < RB / 2) {
+        d = b3_merge(lds[2 * t], lds[2 * t + 1]);
+        nodes[n / 2 + (u64)blockIdx.x * (RB / 2) + t] = d;
+    }
+    __syncthreads();
+    if (t < RB / 2) lds[t] = d;
+    __syncthreads();
+    if (t < RB / 4) nodes[n / 4 + (u64)blockIdx.x * (RB / 4) + t] = b3_merge(lds[2 * t], lds[2 * t + 1]);
+}
 // openings: recompute the local subtree heaps of selected rows; entry e = proof << logn | m. One
 // lane per leaf (coset t of row m, 2^LOGB lanes per entry inside a wave): the leaf, then LOGB
 // merge levels with the right child taken from lane l ^ 2^(k-1) -- 1 + LOGB dependent compressions
@@ -325,6 +362,15 @@ static int up_wmin(u64 T) { return (int)std::min<u64>(T, 64); }
 u64 launch_leaves_lde(const u64* lde, int nc, Digest* nodes, u64 node_stride, int npoly, int logn, int logbeta,
                       hipStream_t s) {
     const u64 n = 1ULL << logn, T = std::min<u64>(256, n / 2);
+    if (n >= 1024 && logbeta >= 1 && (u64)npoly * (n / 256) < 1024) {  // under one wave per SIMD
+        const int logl = logbeta < LEAF_LANES_LOG ? logbeta : LEAF_LANES_LOG;
+        dim3 g((unsigned)(n >> (8 - logl)), npoly), b(256);
+        if (nc == 7) { XFG_LOGB_DISPATCH(leaves_row2_kernel, 7, logbeta, g, b, 0, s, lde, nodes, node_stride, logn) }
+        else if (nc == 2) { XFG_LOGB_DISPATCH(leaves_row2_kernel, 2, logbeta, g, b, 0, s, lde, nodes, node_stride, logn) }
+        else { XFG_LOGB_DISPATCH(leaves_row2_kernel, 1, logbeta, g, b, 0, s, lde, nodes, node_stride, logn) }
+        XFG_CHECK_LAUNCH();
+        return n / 4;
+    }
     if (n >= 1024) {
         dim3 g((unsigned)(n / 256), npoly), b(256);
         if (nc == 7) { XFG_LOGB_DISPATCH(leaves_row_kernel, 7, logbeta, g, b, 0, s, lde, nodes, node_stride, logn) }
