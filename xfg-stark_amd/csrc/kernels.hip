@@ -489,10 +489,45 @@ __global__ __launch_bounds__(256) void tree_mid_kernel(Digest* nodes_all, u64 no
     nodes[count / 2 + i] = d;
     block_tree_up(d, nodes, count / 2, lds, TREE_MID_WMIN);
 }
+// the same three levels for small launch sets (under one block per CU: a lone proof's trees), four lanes
+// per parent (b3_merge_quad): 128 nodes in, 16 out per block, each level's latency about half
+__global__ __launch_bounds__(256) void tree_mid4_kernel(Digest* nodes_all, u64 node_stride, u64 count) {
+    __shared__ Digest lds[64];
+    Digest* nodes = nodes_all + (u64)blockIdx.y * node_stride;
+    const int tid = threadIdx.x, i = tid >> 2, q = tid & 3;
+    u64 c = count, first = (u64)blockIdx.x * 64;  // level being merged; this block's first parent in it
+    for (int w = 64; w >= 16; w >>= 1, c >>= 1, first >>= 1) {
+        const bool act = i < w;  // whole quads
+        uint2 o = make_uint2(0, 0);
+        if (act) {
+            const Digest* src = w == 64 ? nodes + c + 2 * (first + i) : lds + 2 * i;
+            uint32_t m[16];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                m[k] = src[0].w[k];
+                m[8 + k] = src[1].w[k];
+            }
+            o = b3_merge_quad(m, q);
+        }
+        __syncthreads();
+        if (act) {
+            lds[i].w[q] = o.x;
+            lds[i].w[4 + q] = o.y;
+            Digest* dst = nodes + c / 2 + first + i;
+            dst->w[q] = o.x;
+            dst->w[4 + q] = o.y;
+        }
+        __syncthreads();
+    }
+}
 void launch_tree_top(Digest* nodes, u64 node_stride, u64 count, int npoly, hipStream_t s, const CoinStep& cs) {
     while (count > 512) {
-        hipLaunchKernelGGL(tree_mid_kernel, dim3((unsigned)(count / 512), npoly), dim3(256), 0, s, nodes, node_stride,
-                           count);
+        if ((count / 512) * (u64)npoly < 256)
+            hipLaunchKernelGGL(tree_mid4_kernel, dim3((unsigned)(count / 128), npoly), dim3(256), 0, s, nodes,
+                               node_stride, count);
+        else
+            hipLaunchKernelGGL(tree_mid_kernel, dim3((unsigned)(count / 512), npoly), dim3(256), 0, s, nodes,
+                               node_stride, count);
         count /= TREE_MID_SHRINK;
     }
     if (count > 1 || cs.kind != CoinStep::NONE) {
