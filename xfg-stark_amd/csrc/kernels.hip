@@ -30,6 +30,74 @@ __device__ __forceinline__ u64 tw_ipow(const Tables& T, int k, u64 e) {
     return T.tw[(M - ((e << (T.LM - k)) & (M - 1))) & (M - 1)];
 }
 
+// One Merkle parent BLAKE3(l || r) (one 64-byte block: CHUNK_START | CHUNK_END | ROOT, counter 0) computed
+// by the four lanes of a quad: lane q holds column q of the state (s[q], s[4 + q], s[8 + q], s[12 + q]) and
+// all 16 message words. The column half is lane q's G function on its own column; for the diagonal half
+// rows 1-3 rotate by 1, 2, 3 lanes (DPP quad_perm, the compiler's hazard padding) so that lane q holds
+// s[q], s[4 + (q+1)%4], s[8 + (q+2)%4], s[12 + (q+3)%4], and rotate back after it. Each lane picks its
+// G's two message words of the round by a 4-way select. ~330 VALU per lane on the critical path instead of
+// one lane's ~680: the serial top levels of a tree (one compression per level) finish about twice as
+// fast, at four lanes per node. Returns (out[q], out[4 + q]).
+__device__ __forceinline__ uint32_t sel4(bool b0, bool b1, uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
+    return b1 ? (b0 ? x3 : x2) : (b0 ? x1 : x0);
+}
+template <int CTRL>
+__device__ __forceinline__ uint32_t quad_perm(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+}
+constexpr int QP_ROT1 = 0x39, QP_ROT2 = 0x4E, QP_ROT3 = 0x93;  // lane q reads lane (q + k) % 4
+#define XFG_B3_GQ(a, b, c, d, x, y)               \
+    do {                                          \
+        a = b3_add3(a, b, (x));                   \
+        d = b3_rotr(b3_xor(d, a), 16);            \
+        c = b3_add(c, d);                         \
+        b = b3_rotr(b3_xor(b, c), 12);            \
+        a = b3_add3(a, b, (y));                   \
+        d = b3_rotr(b3_xor(d, a), 8);             \
+        c = b3_add(c, d);                         \
+        b = b3_rotr(b3_xor(b, c), 7);             \
+    } while (0)
+// (any chaining value, block length and flags, counter 0: b3_compress_quad; the Merkle parent: b3_merge_quad)
+__device__ __forceinline__ uint2 b3_compress_quad(const uint32_t cv[8], uint32_t m[16], uint32_t len, uint32_t flags,
+                                                  int q) {
+    const bool q0 = q & 1, q1 = (q & 2) != 0;
+    uint32_t a = sel4(q0, q1, cv[0], cv[1], cv[2], cv[3]);
+    uint32_t b = sel4(q0, q1, cv[4], cv[5], cv[6], cv[7]);
+    uint32_t c = sel4(q0, q1, XFG_B3_IV0, XFG_B3_IV1, XFG_B3_IV2, XFG_B3_IV3);
+    uint32_t d = sel4(q0, q1, 0u, 0u, len, flags);
+#pragma unroll
+    for (int r = 0; r < 7; r++) {
+        XFG_B3_GQ(a, b, c, d, sel4(q0, q1, m[0], m[2], m[4], m[6]), sel4(q0, q1, m[1], m[3], m[5], m[7]));
+        b = quad_perm<QP_ROT1>(b);
+        c = quad_perm<QP_ROT2>(c);
+        d = quad_perm<QP_ROT3>(d);
+        XFG_B3_GQ(a, b, c, d, sel4(q0, q1, m[8], m[10], m[12], m[14]), sel4(q0, q1, m[9], m[11], m[13], m[15]));
+        b = quad_perm<QP_ROT3>(b);
+        c = quad_perm<QP_ROT2>(c);
+        d = quad_perm<QP_ROT1>(d);
+        if (r < 6) XFG_B3_PERMUTE(m);
+    }
+    return make_uint2(a ^ c, b ^ d);
+}
+__device__ __forceinline__ uint2 b3_merge_quad(uint32_t m[16], int q) {
+    const uint32_t iv[8] = {XFG_B3_IV0, XFG_B3_IV1, XFG_B3_IV2, XFG_B3_IV3, XFG_B3_IV4, XFG_B3_IV5, XFG_B3_IV6, XFG_B3_IV7};
+    return b3_compress_quad(iv, m, 64, B3_CHUNK_START | B3_CHUNK_END | B3_ROOT, q);
+}
+// a wave-uniform compression (every lane holding the same block: the transcript steps) split over each
+// quad as above, the eight output words then broadcast to the quad's lanes (DPP quad_perm [k,k,k,k])
+__device__ __forceinline__ void b3_compress_uniform(const uint32_t cv[8], uint32_t m[16], uint32_t len, uint32_t flags,
+                                                    uint32_t out[8]) {
+    const uint2 o = b3_compress_quad(cv, m, len, flags, (int)(threadIdx.x & 3));
+    out[0] = quad_perm<0x00>(o.x);
+    out[1] = quad_perm<0x55>(o.x);
+    out[2] = quad_perm<0xAA>(o.x);
+    out[3] = quad_perm<0xFF>(o.x);
+    out[4] = quad_perm<0x00>(o.y);
+    out[5] = quad_perm<0x55>(o.y);
+    out[6] = quad_perm<0xAA>(o.y);
+    out[7] = quad_perm<0xFF>(o.y);
+}
+
 // ============================================================================ device transcript
 // winter-crypto DefaultRandomCoin<Blake3_256> on the device (host twin: host_common.hpp Coin). The
 // transcript steps run inside the kernels that produce their inputs: the coefficient, OOD-point and
@@ -45,6 +113,20 @@ __device__ __forceinline__ Digest dev_merge_int(const Digest& seed, u64 v) {
     for (int i = 10; i < 16; i++) m[i] = 0;
     return b3_hash_block<0xFC00u>(m, 40);  // words 10..15 are zero
 }
+// the same for a (seed, v) every lane of the wave holds: four lanes per compression (b3_compress_uniform)
+__device__ __forceinline__ Digest dev_merge_int_uniform(const Digest& seed, u64 v) {
+    const uint32_t iv[8] = {XFG_B3_IV0, XFG_B3_IV1, XFG_B3_IV2, XFG_B3_IV3, XFG_B3_IV4, XFG_B3_IV5, XFG_B3_IV6, XFG_B3_IV7};
+    uint32_t m[16];
+#pragma unroll
+    for (int i = 0; i < 8; i++) m[i] = seed.w[i];
+    m[8] = (uint32_t)v;
+    m[9] = (uint32_t)(v >> 32);
+#pragma unroll
+    for (int i = 10; i < 16; i++) m[i] = 0;
+    Digest d;
+    b3_compress_uniform(iv, m, 40, B3_CHUNK_START | B3_CHUNK_END | B3_ROOT, d.w);
+    return d;
+}
 // acceptance of a drawn candidate (counter, first two LE words): every element < p
 struct AcceptP {
     __device__ bool operator()(u64, u64 x, u64 y, int D) const { return x < P && (D == 1 || y < P); }
@@ -53,7 +135,7 @@ struct AcceptP {
 template <class A = AcceptP>
 __device__ __forceinline__ bool dev_draw_e(DevCoin& c, u64* out, int D, A acc = A()) {
     for (int i = 0; i < 1000; i++) {
-        const Digest v = dev_merge_int(c.seed, ++c.counter);
+        const Digest v = dev_merge_int_uniform(c.seed, ++c.counter);
         const u64 x = (u64)v.w[0] | ((u64)v.w[1] << 32), y = (u64)v.w[2] | ((u64)v.w[3] << 32);
         if (acc(c.counter, x, y, D)) {
             out[0] = x;
@@ -64,10 +146,18 @@ __device__ __forceinline__ bool dev_draw_e(DevCoin& c, u64* out, int D, A acc = 
     return false;
 }
 __device__ __forceinline__ void dev_reseed(DevCoin& c, const Digest& d) {
-    c.seed = b3_merge(c.seed, d);
+    const uint32_t iv[8] = {XFG_B3_IV0, XFG_B3_IV1, XFG_B3_IV2, XFG_B3_IV3, XFG_B3_IV4, XFG_B3_IV5, XFG_B3_IV6, XFG_B3_IV7};
+    uint32_t m[16];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        m[i] = c.seed.w[i];
+        m[8 + i] = d.w[i];
+    }
+    b3_compress_uniform(iv, m, 64, B3_CHUNK_START | B3_CHUNK_END | B3_ROOT, c.seed.w);
     c.counter = 0;
 }
-// Blake3_256::hash_elements of cnt <= 128 elements: one chunk of ceil(8 cnt / 64) blocks
+// Blake3_256::hash_elements of cnt <= 128 elements: one chunk of ceil(8 cnt / 64) blocks. Like dev_reseed and
+// dev_draw_e, called by a whole wave with the same inputs in every lane (four lanes per compression)
 __device__ Digest dev_hash_elems(const u64* e, int cnt) {
     uint32_t cv[8] = {XFG_B3_IV0, XFG_B3_IV1, XFG_B3_IV2, XFG_B3_IV3, XFG_B3_IV4, XFG_B3_IV5, XFG_B3_IV6, XFG_B3_IV7};
     const int len = 8 * cnt, nb = (len + 63) / 64;
@@ -84,7 +174,7 @@ __device__ Digest dev_hash_elems(const u64* e, int cnt) {
         const bool last = blk == nb - 1;
         const uint32_t flags = (blk == 0 ? B3_CHUNK_START : 0u) | (last ? B3_CHUNK_END | B3_ROOT : 0u);
         uint32_t out[8];
-        b3_compress(cv, m, last ? (uint32_t)(len - 64 * blk) : 64u, 0, flags, out);
+        b3_compress_uniform(cv, m, last ? (uint32_t)(len - 64 * blk) : 64u, flags, out);
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             cv[i] = out[i];
@@ -395,54 +485,6 @@ void launch_open_rows(const u64* lde, int nc, const u64* entries, u64 count, Dig
     else if (nc == 2) { XFG_LOGB_DISPATCH(open_rows_kernel, 2, logbeta, g, b, 0, s, lde, entries, count, out, logn) }
     else { XFG_LOGB_DISPATCH(open_rows_kernel, 1, logbeta, g, b, 0, s, lde, entries, count, out, logn) }
     XFG_CHECK_LAUNCH();
-}
-
-// One Merkle parent BLAKE3(l || r) (one 64-byte block: CHUNK_START | CHUNK_END | ROOT, counter 0) computed
-// by the four lanes of a quad: lane q holds column q of the state (s[q], s[4 + q], s[8 + q], s[12 + q]) and
-// all 16 message words. The column half is lane q's G function on its own column; for the diagonal half
-// rows 1-3 rotate by 1, 2, 3 lanes (DPP quad_perm, the compiler's hazard padding) so that lane q holds
-// s[q], s[4 + (q+1)%4], s[8 + (q+2)%4], s[12 + (q+3)%4], and rotate back after it. Each lane picks its
-// G's two message words of the round by a 4-way select. ~330 VALU per lane on the critical path instead of
-// one lane's ~680: the serial top levels of a tree (one compression per level) finish about twice as
-// fast, at four lanes per node. Returns (out[q], out[4 + q]).
-__device__ __forceinline__ uint32_t sel4(bool b0, bool b1, uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
-    return b1 ? (b0 ? x3 : x2) : (b0 ? x1 : x0);
-}
-template <int CTRL>
-__device__ __forceinline__ uint32_t quad_perm(uint32_t x) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
-}
-constexpr int QP_ROT1 = 0x39, QP_ROT2 = 0x4E, QP_ROT3 = 0x93;  // lane q reads lane (q + k) % 4
-#define XFG_B3_GQ(a, b, c, d, x, y)               \
-    do {                                          \
-        a = b3_add3(a, b, (x));                   \
-        d = b3_rotr(b3_xor(d, a), 16);            \
-        c = b3_add(c, d);                         \
-        b = b3_rotr(b3_xor(b, c), 12);            \
-        a = b3_add3(a, b, (y));                   \
-        d = b3_rotr(b3_xor(d, a), 8);             \
-        c = b3_add(c, d);                         \
-        b = b3_rotr(b3_xor(b, c), 7);             \
-    } while (0)
-__device__ __forceinline__ uint2 b3_merge_quad(uint32_t m[16], int q) {
-    const bool q0 = q & 1, q1 = (q & 2) != 0;
-    uint32_t a = sel4(q0, q1, XFG_B3_IV0, XFG_B3_IV1, XFG_B3_IV2, XFG_B3_IV3);
-    uint32_t b = sel4(q0, q1, XFG_B3_IV4, XFG_B3_IV5, XFG_B3_IV6, XFG_B3_IV7);
-    uint32_t c = a;
-    uint32_t d = sel4(q0, q1, 0u, 0u, 64u, B3_CHUNK_START | B3_CHUNK_END | B3_ROOT);
-#pragma unroll
-    for (int r = 0; r < 7; r++) {
-        XFG_B3_GQ(a, b, c, d, sel4(q0, q1, m[0], m[2], m[4], m[6]), sel4(q0, q1, m[1], m[3], m[5], m[7]));
-        b = quad_perm<QP_ROT1>(b);
-        c = quad_perm<QP_ROT2>(c);
-        d = quad_perm<QP_ROT3>(d);
-        XFG_B3_GQ(a, b, c, d, sel4(q0, q1, m[8], m[10], m[12], m[14]), sel4(q0, q1, m[9], m[11], m[13], m[15]));
-        b = quad_perm<QP_ROT3>(b);
-        c = quad_perm<QP_ROT2>(c);
-        d = quad_perm<QP_ROT1>(d);
-        if (r < 6) XFG_B3_PERMUTE(m);
-    }
-    return make_uint2(a ^ c, b ^ d);
 }
 
 // last levels (count <= 512): one block per tree, four lanes per node (b3_merge_quad), the levels
