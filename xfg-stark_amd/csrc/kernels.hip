@@ -764,12 +764,8 @@ __global__ __launch_bounds__(256) void ood_kernel(const u64* coef, const u64* hc
     const int proof = blockIdx.y, t = threadIdx.x, T = blockDim.x;
     const u64 base = (u64)blockIdx.x * T * OOD_R;
     const F z = F::load(zpts + (u64)proof * 2 * D), zg = F::load(zpts + (u64)proof * 2 * D + D);
-    if (t == 0) {
-        fe_pow(z, base).store(zb[0]);
-        fe_pow(zg, base).store(zb[1]);
-        fe_pow(z, (u64)T).store(zb[2]);
-        fe_pow(zg, (u64)T).store(zb[3]);
-    }
+    for (int k = t; k < 4; k += T)  // the block's four start powers on four threads (a lone proof waits on them)
+        fe_pow(k & 1 ? zg : z, k < 2 ? base : (u64)T).store(zb[k]);
     __syncthreads();
     F pz = fe_mul(F::load(zb[0]), fe_pow(z, (u64)t)), pzg = fe_mul(F::load(zb[1]), fe_pow(zg, (u64)t));
     const F zT = F::load(zb[2]), zgT = F::load(zb[3]);
