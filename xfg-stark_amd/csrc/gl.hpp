@@ -262,7 +262,19 @@ __host__ __device__ inline u64 gl_pow(u64 b, u64 e) {
     }
     return r;
 }
-__host__ __device__ inline u64 gl_inv(u64 a) { return gl_pow(a, P - 2); }
+// a^(p - 2) = 1 / a (0 for a = 0) by an addition chain over x_k = a^(2^k - 1), x_(m+n) = x_m^(2^n) x_n:
+// p - 2 = (2^32 - 2) 2^32 + (2^32 - 1), so 63 squarings and 9 multiplies instead of square-and-multiply's
+// 63 + 62 (the device runs one in each proof's DEEP transcript step)
+__host__ __device__ inline u64 gl_sqn(u64 x, int k) {
+    for (int i = 0; i < k; i++) x = gl_mul(x, x);
+    return x;
+}
+__host__ __device__ inline u64 gl_inv(u64 a) {
+    const u64 x2 = gl_mul(gl_sqn(a, 1), a), x3 = gl_mul(gl_sqn(x2, 1), a), x6 = gl_mul(gl_sqn(x3, 3), x3);
+    const u64 x12 = gl_mul(gl_sqn(x6, 6), x6), x24 = gl_mul(gl_sqn(x12, 12), x12), x30 = gl_mul(gl_sqn(x24, 6), x6);
+    const u64 x31s = gl_sqn(gl_mul(gl_sqn(x30, 1), a), 1);  // a^(2^32 - 2)
+    return gl_mul(gl_sqn(x31s, 32), gl_mul(x31s, a));
+}
 // winter-math get_root_of_unity(k): primitive 2^k-th root
 __host__ __device__ inline u64 gl_root(unsigned k) { return gl_pow(TWO_ADIC_ROOT, 1ULL << (32 - k)); }
 
